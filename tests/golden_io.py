@@ -1,0 +1,91 @@
+"""Loader for the golden fixtures in tests/golden/ (data produced by tests/golden/gen_golden.py)."""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+
+import numpy as np
+import torch
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+# config_parser.py defaults for the flags the path reads (config_parser.py:79-103,123)
+DEFAULT_ARGS = dict(gradient_policy=None, learning_rate=0.05, min_learning_rate=5e-5, decay_factor=0.98,
+                    decay_round=10, yogi_eta=3e-3, yogi_tau=1e-8, yogi_beta=0.9, yogi_beta2=0.99,
+                    qfed_q=1.0, max_staleness=5)
+
+
+def scenario_names():
+    return sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "*.json")))
+
+
+class Scenario:
+    def __init__(self, name):
+        self.name = name
+        with open(os.path.join(GOLDEN, name + ".json")) as f:
+            self.meta = json.load(f)
+        z = np.load(os.path.join(GOLDEN, name + ".npz"))  # allow_pickle defaults to False
+        self.arrays = {k: z[k] for k in z.files}
+        self.names = self.meta["names"]
+        self.T = len(self.names)
+
+    def _tensors(self, prefix):
+        return [self.arrays[f"{prefix}/{i}"] for i in range(self.T)]
+
+    def init_state(self):
+        return [torch.from_numpy(np.array(a)) for a in self._tensors("init")]
+
+    def expected(self, r):
+        return self._tensors(f"out/{r}")
+
+    def yogi_state(self, r):
+        return self._tensors(f"yogi_m/{r}"), self._tensors(f"yogi_v/{r}")
+
+    def client(self, k):
+        vals = []
+        for a in self._tensors(f"client/{k}"):
+            vals.append(a.astype(np.float32) if a.dtype == np.float16 else a)
+        every = self.meta.get("dict_every")
+        if every and k % every == 0:
+            return dict(zip(self.names, vals))
+        return vals
+
+    def rounds(self):
+        """yield (round_index, [client k global indices])"""
+        k0 = 0
+        for r, K in enumerate(self.meta["rounds"]):
+            yield r, list(range(k0, k0 + K))
+            k0 += K
+
+    def args(self):
+        a = dict(DEFAULT_ARGS)
+        a["gradient_policy"] = self.meta.get("optimizer") if self.meta.get("optimizer") not in ("none",) else None
+        if self.meta["policy"] == "q-fedavg":
+            a["qfed_q"] = self.meta["q"]
+            a["learning_rate"] = self.meta["lrs"][0]
+        return argparse.Namespace(**a)
+
+    def results(self, ks, r=0):
+        losses = self.meta.get("losses")
+        out = []
+        for k in ks:
+            out.append({"client_id": k + 1 if self.meta["policy"] != "fedbuff" else 101 + k,
+                        "update_weight": self.client(k),
+                        "moving_loss": float(losses[k]) if losses else 1.0,
+                        "utility": 1.0, "trained_size": 20, "success": True, "wall_duration": 0.0})
+        return out
+
+
+def assert_state_equal(got, want, ctx=""):
+    assert len(got) == len(want), ctx
+    for i, (g, w) in enumerate(zip(got, want)):
+        g = g.detach().cpu().numpy() if torch.is_tensor(g) else np.asarray(g)
+        w = np.asarray(w)
+        assert g.dtype == w.dtype, f"{ctx} tensor {i}: dtype {g.dtype} != {w.dtype}"
+        assert g.shape == w.shape, f"{ctx} tensor {i}: shape {g.shape} != {w.shape}"
+        if not np.array_equal(g, w):
+            bad = np.argwhere(g != w)
+            raise AssertionError(f"{ctx} tensor {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}: "
+                                 f"got {g[tuple(bad[0])] if g.ndim else g} want {w[tuple(bad[0])] if w.ndim else w}")

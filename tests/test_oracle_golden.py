@@ -1,0 +1,35 @@
+"""The CPU oracle (oracle/cpu_reference.py) is bit-exact against every golden fixture that the real
+reference produced (tests/golden/gen_golden.py). CPU only."""
+import pytest
+
+from oracle.cpu_reference import (OracleAggregator, OracleModel, OracleModelAdapter,
+                                  OracleServerOptimizer)
+from tests.golden_io import Scenario, assert_state_equal, scenario_names
+
+
+@pytest.mark.parametrize("name", scenario_names())
+def test_oracle_matches_reference_fixture(name):
+    sc = Scenario(name)
+    args = sc.args()
+    model = OracleModel(sc.names, sc.init_state())
+    policy = sc.meta["policy"]
+    opt = None
+    if sc.meta.get("optimizer") is not None:
+        opt = OracleServerOptimizer(args.gradient_policy, args, None)
+    adapter = OracleModelAdapter(model, optimizer=opt)
+    agg = OracleAggregator(adapter, args, asynchronous=(policy == "fedbuff"))
+    if policy == "fedbuff":
+        agg.round = sc.meta["round"]
+        for k, s in enumerate(sc.meta["staleness"]):
+            agg.client_task_model_version[101 + k] = agg.round - s
+    for r, ks in sc.rounds():
+        if policy == "q-fedavg":
+            args.learning_rate = sc.meta["lrs"][r]
+        agg.start_round(len(ks))
+        for res in sc.results(ks, r):
+            agg.on_result(res)
+        assert_state_equal(adapter.get_weights(), sc.expected(r), f"{name} round {r}")
+        if policy == "fed-yogi":
+            m, v = sc.yogi_state(r)
+            assert_state_equal(opt.gradient_controller.m_t, m, f"{name} m round {r}")
+            assert_state_equal(opt.gradient_controller.v_t, v, f"{name} v round {r}")
