@@ -1,0 +1,213 @@
+"""Benchmark: device-resident FedAvg reduction of K x P fp32 client updates on MI355X.
+
+Workload (BASELINE.json north_star target): K = 1000 clients x P = 25,000,000 fp32 parameters per GPU,
+FedAvg (aggregator.py:489-511): out = (sum of the K updates in arrival order) / K, one fused HIP kernel
+(fa_reduce, FA_FINALIZE).  Inputs are generated on the device before the timed region and stay in HBM.
+
+A "step" is one aggregation round over the resident K x P batch.  With --gpus N (one process per GPU,
+torchrun) every rank owns an equal 25M-parameter shard of an N x 25M-parameter model and reduces its
+K client slices: weak scaling, no data-path collective.  ``value`` counts client updates of one 25M-fp32
+(100 MB) slice across all ranks per second.  --reassemble additionally times the RCCL all-gather that
+rebuilds the global model for egress (reported as ``reassembly_ms``, not part of ``value``).
+
+Extra objects on the JSON line:
+  roofline     achieved algorithmic GB/s of the reduce kernel (4KP+4P bytes per launch / mean launch time
+               from HIP events on the launch stream) vs the 8 TB/s HBM3E peak; ``traffic`` = HBM bytes
+               per launch from the rocprofv3 PMC summary committed under profiles/ (null if absent)
+  cpu_baseline the CPU oracle (numpy restatement of aggregator.py:497-507, bit-exact to the reference's
+               golden vectors) timed on this host on a bounded sample of the same workload (rank 0, N=1)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clients", type=int, default=1000)
+    ap.add_argument("--params", type=int, default=25_000_000, help="fp32 parameters per GPU shard")
+    ap.add_argument("--policy", default="fedavg", choices=["fedavg", "fedyogi", "fedbuff"])
+    ap.add_argument("--reassemble", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample (0 = skip)")
+    ap.add_argument("--seed", type=int, default=2024)
+    return ap.parse_args()
+
+
+def cpu_baseline(K: int, P: int, budget_s: float, seed: int) -> dict:
+    """Time the oracle's FedAvg restatement on host cores on a K-subsample, extrapolated to K."""
+    import numpy as np
+
+    from oracle.cpu_reference import fedavg_close, fedavg_step
+
+    rng = np.random.default_rng(seed)
+    pool_n = 8
+    base = rng.standard_normal(P, dtype=np.float32) * np.float32(0.05)
+    pool = [base + rng.standard_normal(P, dtype=np.float32) * np.float32(0.01) for _ in range(pool_n)]
+    # per-client accumulate cost (aggregator.py:500-503: one numpy add per tensor, new array each time)
+    acc = fedavg_step(None, [pool[0]], True)
+    n = 0
+    t0 = time.perf_counter()
+    while True:
+        acc = fedavg_step(acc, [pool[(n + 1) % pool_n]], False)
+        n += 1
+        if time.perf_counter() - t0 > budget_s * 0.8 or n >= K - 1:
+            break
+    t_acc = (time.perf_counter() - t0) / n
+    t1 = time.perf_counter()
+    fedavg_close(acc, K)
+    t_fin = time.perf_counter() - t1
+    t_round = t_acc * (K - 1) + t_fin
+    return {"value": K / t_round, "unit": "client-updates/s", "cores": 1, "kind": "port",
+            "sample": f"oracle FedAvg (numpy, single-threaded) over {n + 1} of the {K} x {P} fp32 client updates "
+                      f"(pool of {pool_n} distinct 100 MB buffers), {t_acc * 1e3:.1f} ms/client + "
+                      f"{t_fin * 1e3:.0f} ms finalize, extrapolated linearly to K={K}",
+            "host": platform.processor() or platform.machine(), "host_cpus": os.cpu_count()}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from fedscale_amd import kernels as kx
+    from fedscale_amd import synth
+    from fedscale_amd.bucket import round_up
+
+    K, P = args.clients, args.params
+    ld = round_up(P, 64)
+    x = torch.empty(K, ld, dtype=torch.float32, device=dev)
+    synth.fill(x, K, P, seed=args.seed + 7919 * rank)
+    out = torch.zeros(ld, dtype=torch.float32, device=dev)
+    denom = float(np.float32(K))
+    yogi = None
+    if args.policy == "fedyogi":
+        yogi = dict(last=torch.zeros(ld, device=dev), m=torch.zeros(ld, device=dev), v=torch.zeros(ld, device=dev),
+                    eta=float(np.float32(3e-3)), tau=float(np.float32(1e-8)), beta=float(np.float32(0.9)),
+                    omb=float(np.float32(1 - 0.9)), omb2=float(np.float32(1 - 0.99)), init=False)
+        synth.fill(yogi["last"].view(1, -1), 1, P, seed=args.seed + 1)
+    a = None
+    if args.policy == "fedbuff":
+        s = [1 / (1 + (k % 6)) ** 0.5 for k in range(K)]
+        a = torch.tensor(np.asarray(s, dtype=np.float32), device=dev)
+        denom = float(np.float32(sum(s)))
+    gathered = None
+
+    stream = torch.cuda.current_stream(dev)
+
+    def step(ev=None):
+        if ev is not None:
+            ev[0].record(stream)
+        if yogi is None:
+            kx.reduce(x, K, P, out, a=a, denom=denom, finalize=True)
+        else:
+            kx.reduce_yogi(x, K, P, out=out, denom=denom, **yogi)
+        if ev is not None:
+            ev[1].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(evs[i])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+
+    reassembly_ms = None
+    if args.reassemble and world > 1:
+        gathered = torch.empty(world * ld, dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(gathered, out)
+        torch.cuda.synchronize(dev)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        dist.barrier()
+        e0.record(stream)
+        for _ in range(5):
+            dist.all_gather_into_tensor(gathered, out)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        reassembly_ms = e0.elapsed_time(e1) / 5
+
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall, kern_ms_max = float(t[0]), float(t[1])
+
+    if rank == 0:
+        ms_per_step = wall * 1e3 / args.steps
+        value = world * K * args.steps / wall
+        extra = {"fedavg": 0, "fedbuff": 4 * K, "fedyogi": 20 * P}[args.policy]
+        alg_bytes = 4 * K * P + 4 * P + extra  # SURVEY §8d algorithmic bytes per launch (per GPU)
+        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(PMC_FILE):
+            try:
+                pmc = json.load(open(PMC_FILE))
+                key = f"{args.policy}_k{K}_p{P}"
+                if key in pmc:
+                    traffic = pmc[key]["hbm_bytes_per_launch"]
+            except Exception:
+                traffic = None
+        res = {
+            "metric": "client-updates/s, device-resident FedAvg reduce of K x P fp32 (P per GPU)",
+            "value": value, "unit": "client-updates/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic full-weight client updates (base + noise, hash-generated on device), HBM-resident",
+            "config": {"workload": f"{args.policy}_k{K}_p{P}_per_gpu", "clients": K, "params_per_gpu": P,
+                       "model_params_total": P * world, "policy": args.policy,
+                       "parallelism": f"param-shard x{world} (one process per GPU)"},
+            "hbm_gbps": achieved,
+            "kernel_ms": kern_ms,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "k_reduce (fa_reduce FA_FINALIZE)" if args.policy != "fedyogi" else
+                         "k_reduce EPI_YOGI (fa_reduce_yogi)",
+                         "alg_bytes_per_launch": alg_bytes},
+        }
+        if reassembly_ms is not None:
+            res["reassembly_ms"] = reassembly_ms
+        if world == 1 and args.cpu_seconds > 0:
+            del x
+            torch.cuda.empty_cache()
+            res["cpu_baseline"] = cpu_baseline(K, P, args.cpu_seconds, args.seed)
+        else:
+            res["cpu_baseline"] = None
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

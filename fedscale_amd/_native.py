@@ -1,0 +1,100 @@
+"""ctypes binding of libfedagg.so — the C ABI declared in include/fedagg.h.
+
+This is the only way the package reaches the GPU.  There is no fallback: if the shared library is
+missing or a call fails, a ``FedAggError`` is raised.  Build it with ``python __graft_entry__.py``
+(or ``make -C fedscale_amd/csrc``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, "libfedagg.so"))
+ABI_VERSION = 1
+
+FA_ACCUMULATE = 1
+FA_FINALIZE = 2
+FA_YOGI_INIT = 4
+
+
+class FedAggError(RuntimeError):
+    pass
+
+
+_c_void_p, _i32, _i64, _f32, _f64, _u32 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float,
+                                             ctypes.c_double, ctypes.c_uint32)
+
+# name -> (restype, argtypes);  must list every symbol of include/fedagg.h
+SIGNATURES = {
+    "fa_abi_version": (_i32, []),
+    "fa_last_error_string": (ctypes.c_char_p, []),
+    "fa_reduce": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _f32, _i32, _c_void_p]),
+    "fa_reduce_yogi": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p,
+                              _c_void_p, _c_void_p, _c_void_p, _f32, _f32, _f32, _f32, _f32, _i32, _c_void_p]),
+    "fa_yogi_step": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32, _f32, _f32,
+                            _f32, _i32, _c_void_p]),
+    "fa_qfed_max_chunk": (_i32, []),
+    "fa_qfed_workspace_bytes": (_i64, [_i32]),
+    "fa_qfed_accumulate": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p,
+                                  _c_void_p, _i32, _c_void_p]),
+    "fa_qfed_hs": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p]),
+    "fa_qfed_finalize": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p]),
+    "fa_side_accumulate": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _i32,
+                                  _c_void_p]),
+    "fa_side_close": (_i32, [_c_void_p, _c_void_p, _i32, _i32, _f64, _c_void_p, _c_void_p, _c_void_p]),
+    "fa_side_yogi": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _f64, _f64,
+                            _f64, _f64, _f64, _i32, _c_void_p]),
+    "fa_side_qfed_accumulate": (_i32, [_c_void_p, _i32, _i32, _i32, _c_void_p, _c_void_p, _f32, _c_void_p,
+                                       _c_void_p, _i32, _c_void_p]),
+    "fa_side_qfed_finalize": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p]),
+    "fa_fill_synthetic": (_i32, [_c_void_p, _i64, _i32, _i64, _u32, _i32, _f32, _f32, _c_void_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH):
+    """Load (once) and type the shared library.  Raises FedAggError when it is absent."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise FedAggError(f"{path} not found: the HIP extension is not built "
+                              f"(run `python __graft_entry__.py` to build it; there is no CPU fallback)")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.fa_abi_version()
+        if v != ABI_VERSION:
+            raise FedAggError(f"{path}: ABI version {v}, expected {ABI_VERSION}")
+        _lib = lib
+        return lib
+
+
+def call(name: str, *args):
+    """Call an fa_* entry point; raise on a non-zero return code."""
+    lib = load()
+    rc = getattr(lib, name)(*args)
+    if rc != 0:
+        msg = lib.fa_last_error_string().decode(errors="replace")
+        raise FedAggError(f"{name} failed ({rc}): {msg}")
+    return rc
+
+
+def ptr(t) -> int:
+    """Device pointer of a torch tensor (None -> NULL)."""
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(device=None) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,180 @@
+"""Flat device layout of a state_dict ("bucket") and the client-update staging area.
+
+HBM layout:
+  * fp32 entries of the state_dict, concatenated in state_dict order -> one flat vector of P elements.
+    A rank owns the contiguous slice [p0, p1) of it (balanced, 64-element aligned, equal-size shards so
+    the reassembly is a plain all-gather); its local row stride ``ld`` is P_local rounded up to 64
+    floats (256 B) and the padding is kept at zero.
+  * non-fp32 entries (int64 BatchNorm ``num_batches_tracked`` ...) -> the "side table" of Q int64
+    elements, replicated on every rank (it is a few hundred bytes).
+  * a round's client updates live client-major: x[slot, :] (fp32, [capacity, ld]) and xi[slot, :]
+    (int64, [capacity, Q]).  Positional mapping to state_dict keys follows
+    torch_model_adapter.py:31-34 (weights[i] <-> i-th key).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+ALIGN = 64  # floats: 256-byte rows, and the shard granule
+
+
+def round_up(n: int, m: int) -> int:
+    return (n + m - 1) // m * m
+
+
+@dataclass
+class Entry:
+    index: int
+    name: str
+    shape: Tuple[int, ...]
+    dtype: torch.dtype
+    offset: int  # into the fp32 vector (kind 'f') or the side table (kind 'i')
+    numel: int
+    kind: str  # 'f' fp32 bucket | 'i' int64 side table
+
+
+_SUPPORTED = {torch.float32: "f", torch.int64: "i"}
+
+
+class BucketLayout:
+    def __init__(self, names: Sequence[str], shapes: Sequence[Sequence[int]], dtypes: Sequence[torch.dtype],
+                 rank: int = 0, world: int = 1):
+        if world < 1 or not (0 <= rank < world):
+            raise ValueError(f"bad shard ({rank}, {world})")
+        self.entries: List[Entry] = []
+        pf = pi = 0
+        for i, (n, s, d) in enumerate(zip(names, shapes, dtypes)):
+            if d not in _SUPPORTED:
+                raise NotImplementedError(
+                    f"state_dict entry {n!r} has dtype {d}; the device path supports float32 parameters/buffers "
+                    f"and int64 buffers (FedScale models)")
+            numel = int(np.prod(s)) if len(s) else 1
+            kind = _SUPPORTED[d]
+            e = Entry(i, n, tuple(int(v) for v in s), d, pf if kind == "f" else pi, numel, kind)
+            if kind == "f":
+                pf += numel
+            else:
+                pi += numel
+            self.entries.append(e)
+        self.names = list(names)
+        self.T = len(self.entries)
+        self.P_full = pf
+        self.Q = pi
+        self.rank, self.world = rank, world
+        self.shard = round_up(max(1, -(-pf // world)), ALIGN)  # equal-size shards
+        self.p0 = min(pf, rank * self.shard)
+        self.p1 = min(pf, self.p0 + self.shard)
+        self.P = self.p1 - self.p0
+        self.ld = self.shard  # local row stride (multiple of 64, >= P)
+        self.ldq = max(1, self.Q)
+        self.f_entries = [e for e in self.entries if e.kind == "f"]
+        self.i_entries = [e for e in self.entries if e.kind == "i"]
+
+    @classmethod
+    def from_state_dict(cls, sd, rank: int = 0, world: int = 1) -> "BucketLayout":
+        return cls(list(sd.keys()), [tuple(v.shape) for v in sd.values()], [v.dtype for v in sd.values()],
+                   rank, world)
+
+    def same_structure(self, names, shapes) -> bool:
+        return list(names) == self.names and [tuple(s) for s in shapes] == [e.shape for e in self.entries]
+
+    # ---- host-side packing ----------------------------------------------------------------------
+    def values_of(self, update) -> list:
+        """dict name->array | list -> list in state_dict order (aggregator.py:494-496)."""
+        if type(update) is dict:
+            update = list(update.values())
+        if len(update) != self.T:
+            raise ValueError(f"update has {len(update)} tensors, the model has {self.T}")
+        return update
+
+    def pack_host(self, values: list, f_out: np.ndarray, i_out: np.ndarray):
+        """Copy this rank's slice of the fp32 entries into f_out[:P] and the int entries into i_out[:Q]."""
+        values = self.values_of(values)
+        for e in self.entries:
+            v = values[e.index]
+            if isinstance(v, torch.Tensor):
+                v = v.detach().cpu().numpy()
+            a = np.asarray(v)
+            if tuple(a.shape) != e.shape:
+                raise ValueError(f"{e.name}: shape {tuple(a.shape)} != model shape {e.shape}")
+            if e.kind == "f":
+                if a.dtype != np.float32:
+                    raise TypeError(f"{e.name}: dtype {a.dtype}, the model entry is float32")
+                lo, hi = max(e.offset, self.p0), min(e.offset + e.numel, self.p1)
+                if lo < hi:
+                    f_out[lo - self.p0:hi - self.p0] = a.reshape(-1)[lo - e.offset:hi - e.offset]
+            else:
+                if a.dtype != np.int64:
+                    raise TypeError(f"{e.name}: dtype {a.dtype}, the model entry is int64")
+                i_out[e.offset:e.offset + e.numel] = a.reshape(-1)
+
+    def pack_device(self, values: list, f_dst: torch.Tensor, i_dst: torch.Tensor):
+        """Same as pack_host for a list of tensors already resident on this device (D2D copies)."""
+        values = self.values_of(values)
+        for e in self.entries:
+            v = values[e.index]
+            if not isinstance(v, torch.Tensor):
+                v = torch.as_tensor(np.asarray(v))
+            if tuple(v.shape) != e.shape:
+                raise ValueError(f"{e.name}: shape {tuple(v.shape)} != model shape {e.shape}")
+            if v.dtype != e.dtype:
+                raise TypeError(f"{e.name}: dtype {v.dtype} != model dtype {e.dtype}")
+            flat = v.reshape(-1)
+            if e.kind == "f":
+                lo, hi = max(e.offset, self.p0), min(e.offset + e.numel, self.p1)
+                if lo < hi:
+                    f_dst[lo - self.p0:hi - self.p0].copy_(flat[lo - e.offset:hi - e.offset], non_blocking=True)
+            else:
+                i_dst[e.offset:e.offset + e.numel].copy_(flat, non_blocking=True)
+
+    def unpack(self, f_full: torch.Tensor, i_side: torch.Tensor) -> list:
+        """Views of a FULL (gathered, length >= P_full) fp32 vector + side table as state_dict tensors."""
+        out = []
+        for e in self.entries:
+            src = f_full if e.kind == "f" else i_side
+            out.append(src[e.offset:e.offset + e.numel].view(e.shape))
+        return out
+
+
+class ClientStaging:
+    """Device staging area for up to ``capacity`` client updates of one round (chunk).
+
+    Host -> device ingress goes through a ring of pinned host buffers; each H2D copy is enqueued on the
+    current stream, so stream order guarantees a slot is not overwritten while a kernel still reads it.
+    """
+
+    def __init__(self, layout: BucketLayout, device, capacity: int, ring: int = 2):
+        self.layout = layout
+        self.device = torch.device(device)
+        self.capacity = int(capacity)
+        self.x = torch.zeros(self.capacity, layout.ld, dtype=torch.float32, device=self.device)
+        self.xi = torch.zeros(self.capacity, layout.ldq, dtype=torch.int64, device=self.device)
+        self._ring = []
+        for _ in range(ring):
+            hf = torch.zeros(layout.ld, dtype=torch.float32).pin_memory()
+            hi = torch.zeros(layout.ldq, dtype=torch.int64).pin_memory()
+            self._ring.append([hf, hi, None])
+        self._next = 0
+
+    def put(self, slot: int, update):
+        lay = self.layout
+        values = lay.values_of(update)
+        on_dev = [isinstance(v, torch.Tensor) and v.device == self.device for v in values]
+        if all(on_dev):
+            lay.pack_device(values, self.x[slot], self.xi[slot])
+            return
+        hf, hi, ev = self._ring[self._next]
+        if ev is not None:
+            ev.synchronize()  # the previous H2D out of this pinned buffer has completed
+        lay.pack_host(values, hf.numpy(), hi.numpy())
+        self.x[slot, :lay.P].copy_(hf[:lay.P], non_blocking=True)
+        if lay.Q:
+            self.xi[slot, :lay.Q].copy_(hi[:lay.Q], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.device))
+        self._ring[self._next][2] = ev
+        self._next = (self._next + 1) % len(self._ring)

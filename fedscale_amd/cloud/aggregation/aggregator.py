@@ -1,0 +1,135 @@
+"""Device aggregation hook — drop-in for ``Aggregator.update_weight_aggregation``.
+
+Reference: fedscale/cloud/aggregation/aggregator.py:489-511 (sync FedAvg, + the q-FedAvg retention of
+:466-467 and the server step reached through set_weights, :508-511) and
+fedscale/cloud/aggregation/async_aggregator.py:115-137 (FedBuff).  The plugin API of the reference is
+subclassing ``Aggregator`` and overriding ``update_weight_aggregation(self, results)``
+(precedents: AsyncAggregator, MNN/TFLite aggregators, examples/auxo); so is this::
+
+    from fedscale.cloud.aggregation.aggregator import Aggregator
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregatorMixin
+
+    class MI355XAggregator(DeviceAggregatorMixin, Aggregator):
+        pass
+
+State contract (the reference test's MockAggregator, fedscale/tests/cloud/aggregation/test_aggregator.py:11-17):
+``model_weights, model_in_update, tasks_round, model_wrapper, client_training_results`` (+ ``args``,
+and for FedBuff ``round, client_task_model_version, aggregation_denominator``).  ``model_in_update`` is
+incremented by the caller before the call (aggregator.py:484); the first/last tests are ==1 / ==K
+(:430-434).  ``model_wrapper`` must be a ``fedscale_amd`` TorchModelAdapter.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ..internal.torch_model_adapter import TorchModelAdapter
+
+
+class DeviceAggregatorMixin:
+    #: clients staged per chunk (None: as many as fit in half of the free HBM)
+    device_round_capacity = None
+    #: keep the FedAvg mean as ``model_weights`` in fused fed-yogi rounds (costs P*4 bytes of writes)
+    device_keep_mean = True
+
+    _device_round = None
+
+    # same predicates as aggregator.py:430-434 (defined here too so the mixin also works standalone)
+    def _is_first_result_in_round(self):
+        return self.model_in_update == 1
+
+    def _is_last_result_in_round(self):
+        return self.model_in_update == self.tasks_round
+
+    def init_model(self):
+        """aggregator.py:198-211, re-wired onto the device adapter + device server optimizer."""
+        from .optimizers import TorchServerOptimizer
+
+        super().init_model()
+        model = self.model_wrapper.get_model()
+        self.model_wrapper = TorchModelAdapter(
+            model, optimizer=TorchServerOptimizer(self.args.gradient_policy, self.args, self.device))
+
+    def _wrapper(self) -> TorchModelAdapter:
+        w = self.model_wrapper
+        if not isinstance(w, TorchModelAdapter):
+            raise TypeError(f"model_wrapper is {type(w).__name__}; the device path needs "
+                            f"fedscale_amd.cloud.internal.torch_model_adapter.TorchModelAdapter")
+        return w
+
+    def _device_policy(self) -> str:
+        opt = self._wrapper().optimizer
+        return "qfedavg" if (opt is not None and getattr(opt, "mode", None) == "q-fedavg") else "fedavg"
+
+    def update_weight_aggregation(self, results):
+        w = self._wrapper()
+        if self._is_first_result_in_round() or self._device_round is None:
+            self._device_round = w.begin_round(self.tasks_round, self._device_policy(),
+                                               capacity=self.device_round_capacity)
+        rnd = self._device_round
+        if rnd.policy == "qfedavg":
+            a = w.optimizer.args  # optimizers.py:69 reads the live args at step time
+            rnd.add(results["update_weight"], loss=results["moving_loss"], learning_rate=a.learning_rate,
+                    q=a.qfed_q)
+        else:
+            rnd.add(results["update_weight"])
+        if self._is_last_result_in_round():
+            K = self.tasks_round
+            # np.divide(w, K): fp32 entries divide by fp32(K), int64 sums by float64(K)
+            w.apply_round(rnd, float(np.float32(K)), float(K),
+                          client_training_results=self.client_training_results, keep_mean=self.device_keep_mean)
+            self.model_weights = w.round_mean_weights()
+            self._device_round = None
+
+
+class DeviceAsyncAggregatorMixin(DeviceAggregatorMixin):
+    """FedBuff (async_aggregator.py:115-137): staleness-weighted accumulate, divide by the weight sum."""
+
+    def update_weight_aggregation(self, results):
+        w = self._wrapper()
+        # async_aggregator.py:125-126 — Python-float weight and denominator
+        s = 1 / (1 + self.round - self.client_task_model_version[results["client_id"]]) ** 0.5
+        self.aggregation_denominator += s
+        if self._is_first_result_in_round() or self._device_round is None:
+            self._device_round = w.begin_round(self.tasks_round, "fedbuff", capacity=self.device_round_capacity)
+        self._device_round.add(results["update_weight"], weight=s)
+        if self._is_last_result_in_round():
+            den = self.aggregation_denominator
+            # np.divide(fp32 array, Python float) divides by fp32(den) (NEP 50); float64 sides by den
+            w.apply_round(self._device_round, float(np.float32(den)), float(den), client_training_results=None,
+                          keep_mean=self.device_keep_mean)
+            self.model_weights = w.round_mean_weights()
+            self.aggregation_denominator = 0
+            self._device_round = None
+
+
+class DeviceAggregator(DeviceAggregatorMixin):
+    """Standalone holder of the hot-path state contract (for tools, tests and non-FedScale callers)."""
+
+    def __init__(self, model_wrapper: TorchModelAdapter, args=None):
+        self.model_weights = []
+        self.model_in_update = 0
+        self.tasks_round = 0
+        self.model_wrapper = model_wrapper
+        self.client_training_results = []
+        self.args = args
+
+    def start_round(self, tasks_round: int):
+        """round_completion_handler's reset (aggregator.py:609, 620-623)."""
+        self.tasks_round = tasks_round
+        self.model_in_update = 0
+        self.client_training_results = []
+
+    def on_result(self, results):
+        """client_completion_handler's reduction lines (aggregator.py:466-467, 482-487)."""
+        if self.args is not None and getattr(self.args, "gradient_policy", None) in ["q-fedavg"]:
+            self.client_training_results.append(results)
+        self.model_in_update += 1
+        self.update_weight_aggregation(results)
+
+
+class DeviceAsyncAggregator(DeviceAsyncAggregatorMixin, DeviceAggregator):
+    def __init__(self, model_wrapper: TorchModelAdapter, args=None):
+        DeviceAggregator.__init__(self, model_wrapper, args)
+        self.round = 0
+        self.client_task_model_version = {}
+        self.aggregation_denominator = 0

@@ -1,0 +1,227 @@
+"""Device-resident TorchModelAdapter — drop-in for fedscale/cloud/internal/torch_model_adapter.py:10-53.
+
+The global model lives in HBM as a flat bucket (``fedscale_amd.bucket``), double-buffered: the round's
+result is written into the spare buffer while the current one is the optimizer's ``last_model``
+(torch_model_adapter.py:30 clones it; the ping-pong makes that clone free).  ``self.model`` (the
+nn.Module the reference exposes through ``get_model``) is synchronised from HBM lazily, on egress
+(``get_weights`` / ``get_model``), which is where the reference's pickling of the model happens anyway
+(aggregator.py:788-804, 902-909).
+
+Reference API (same names, argument meaning and error behaviour on valid input):
+    TorchModelAdapter(model, optimizer=None)
+    set_weights(weights, is_aggregator=True, client_training_results=None)
+    get_weights() -> list of CPU tensors (cloned), in state_dict order
+    get_model()   -> the nn.Module holding the current global weights
+Device fast path used by ``DeviceAggregatorMixin``:
+    begin_round(K, policy) -> DeviceRound;  apply_round(round, denom32, denom64, client_training_results)
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ...bucket import BucketLayout, ClientStaging
+from ...round import DeviceRound, default_capacity
+from ...state import FlatState, ShardGroup
+from .model_adapter_base import ModelAdapterBase
+
+
+def _resolve_device(device) -> torch.device:
+    if device is None:
+        return torch.device("cuda", torch.cuda.current_device())
+    d = torch.device(device)
+    if d.type != "cuda":
+        raise ValueError(f"device {d}: the aggregation path runs on the GPU only (no CPU fallback)")
+    if d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
+class TorchModelAdapter(ModelAdapterBase):
+    def __init__(self, model: torch.nn.Module, optimizer=None, device=None, shards: Optional[ShardGroup] = None,
+                 staging_capacity: Optional[int] = None, _load_from=None):
+        self.model = model
+        self.optimizer = optimizer
+        self.device = _resolve_device(device)
+        self.shards = shards or ShardGroup()
+        sd = model.state_dict()
+        self.layout = BucketLayout.from_state_dict(sd, self.shards.rank, self.shards.world)
+        L, dev = self.layout, self.device
+        self._f = [torch.zeros(L.ld, dtype=torch.float32, device=dev) for _ in range(2)]
+        self._s = [torch.zeros(L.ldq, dtype=torch.int64, device=dev) for _ in range(2)]
+        self._cur = 0
+        # float64 side table + fp32 mean of the last round: the reference's Aggregator.model_weights
+        self._mean_s = torch.zeros(L.ldq, dtype=torch.float64, device=dev)
+        self._mean_f: Optional[torch.Tensor] = None
+        self._mean_valid = False
+        self.staging: Optional[ClientStaging] = None
+        self.staging_capacity = staging_capacity
+        cur_f = torch.zeros(L.ld, dtype=torch.float32, device=dev)
+        cur_s = torch.zeros(L.ldq, dtype=torch.float64, device=dev)
+        self._pack_values(list(_load_from) if _load_from is not None else list(sd.values()), cur_f, cur_s)
+        self._f[0].copy_(cur_f)
+        self._s[0].copy_(cur_s.to(torch.int64))
+        self._version = 0  # bumps on every device-side model update
+        self._module_version = 0 if _load_from is None else -1
+
+    # ---- internal buffers ---------------------------------------------------------------------
+    def _snapshot(self) -> FlatState:
+        return FlatState(self.layout, self._f[self._cur], self._s[self._cur])
+
+    def _scratch_buffers(self):
+        return self._f[1 - self._cur], self._s[1 - self._cur]
+
+    def _commit_scratch(self):
+        self._cur = 1 - self._cur
+        self._version += 1
+
+    def _sqnorm_allreduce(self):
+        return self.shards.all_reduce_sum if self.shards.world > 1 else None
+
+    def _pack_values(self, values: list, f_dst: torch.Tensor, s_dst: torch.Tensor):
+        """weights list -> device fp32 bucket slice + side table (converted to s_dst's dtype)."""
+        L = self.layout
+        values = L.values_of(values)
+        for e in L.entries:
+            v = values[e.index]
+            t = v.detach() if isinstance(v, torch.Tensor) else torch.as_tensor(np.asarray(v))
+            if tuple(t.shape) != e.shape:
+                raise ValueError(f"{e.name}: shape {tuple(t.shape)} != model shape {e.shape}")
+            flat = t.reshape(-1)
+            if e.kind == "f":
+                lo, hi = max(e.offset, L.p0), min(e.offset + e.numel, L.p1)
+                if lo < hi:
+                    # np.asarray(w, dtype=float32) (torch_model_adapter.py:32)
+                    f_dst[lo - L.p0:hi - L.p0].copy_(flat[lo - e.offset:hi - e.offset].to(torch.float32))
+            else:
+                s_dst[e.offset:e.offset + e.numel].copy_(flat.to(s_dst.dtype))
+
+    # ---- reference API --------------------------------------------------------------------------
+    def set_weights(self, weights, is_aggregator=True, client_training_results=None):
+        """torch_model_adapter.py:23-39 on the device."""
+        L = self.layout
+        last = self._snapshot()
+        cur_f = torch.zeros(L.ld, dtype=torch.float32, device=self.device)
+        cur_s = torch.zeros(L.ldq, dtype=torch.float64, device=self.device)
+        self._pack_values(list(weights), cur_f, cur_s)
+        self._mean_f, self._mean_s, self._mean_valid = cur_f, cur_s, True
+        opt = self.optimizer
+        if opt is not None and is_aggregator and getattr(opt, "mode", None) in ("fed-yogi", "q-fedavg"):
+            opt.update_round_gradient(last, FlatState(L, cur_f, cur_s), self, client_training_results)
+            return
+        nf, ns = self._scratch_buffers()
+        nf.copy_(cur_f)
+        ns.copy_(cur_s.to(torch.float32).to(torch.int64))  # float32 -> int64 load truncates (:31-35)
+        self._commit_scratch()
+
+    def get_weights(self) -> List[torch.Tensor]:
+        """torch_model_adapter.py:41-47: cloned CPU tensors in state_dict order (gathers the shards)."""
+        L = self.layout
+        full = self.shards.all_gather(self._f[self._cur])
+        f_cpu = full[:L.P_full].to("cpu")
+        s_cpu = self._s[self._cur][:L.Q].to("cpu")
+        return [t.clone() for t in L.unpack(f_cpu, s_cpu)]
+
+    def get_model(self):
+        if self._module_version != self._version:
+            sd = self.model.state_dict()
+            self.model.load_state_dict({n: t for n, t in zip(sd.keys(), self.get_weights())})
+            self._module_version = self._version
+        return self.model
+
+    # ---- device fast path -----------------------------------------------------------------------
+    def begin_round(self, K: int, policy: str, capacity: Optional[int] = None) -> DeviceRound:
+        cap = capacity or self.staging_capacity
+        want = min(cap or default_capacity(self.layout, K, self.device), K)
+        if self.staging is None or self.staging.capacity < want:
+            self.staging = None
+            self.staging = ClientStaging(self.layout, self.device, want)
+        snap = self._snapshot()
+        return DeviceRound(self.layout, self.device, K, policy, capacity=want, staging=self.staging,
+                           last_f32=snap.f32, last_i64=snap.side)
+
+    def apply_round(self, rnd: DeviceRound, denom32: float, denom64: float, client_training_results=None,
+                    keep_mean: bool = True):
+        """Finish a round: reduce the last chunk with the server step fused, then swap buffers."""
+        L = self.layout
+        last = self._snapshot()
+        out_f, out_s = self._scratch_buffers()
+        opt = self.optimizer
+        mode = getattr(opt, "mode", None) if opt is not None else None
+        if rnd.policy == "qfedavg":
+            if mode != "q-fedavg":
+                raise RuntimeError("a q-FedAvg round needs the q-fedavg server optimizer")
+            rnd.finalize_qfed(out=out_f, model_side=out_s, sqnorm_allreduce=self._sqnorm_allreduce())
+            self._mean_valid = False
+        elif mode == "fed-yogi":
+            y = opt.gradient_controller
+            y.bind(L, self.device)
+            mean_f = None
+            if keep_mean:
+                if self._mean_f is None or self._mean_f is last.f32 or self._mean_f is out_f:
+                    self._mean_f = torch.zeros(L.ld, dtype=torch.float32, device=self.device)
+                mean_f = self._mean_f
+            yargs = y.fused_args(last.f32)
+            yargs["mean_out"] = mean_f
+            rnd.finalize_mean(denom32, denom64, out=out_f, cur_side=self._mean_s, model_side=None, yogi=yargs)
+            y.step_side(self._mean_s, last.side, model=out_s)
+            y.initialized = True
+            self._mean_valid = keep_mean
+        elif mode == "q-fedavg":
+            raise RuntimeError("q-fedavg optimizer but the round was not staged as q-FedAvg")
+        else:
+            rnd.finalize_mean(denom32, denom64, out=out_f, cur_side=self._mean_s, model_side=out_s)
+            self._mean_f = out_f  # FedAvg without a server step: the mean IS the new model
+            self._mean_valid = True
+        self._commit_scratch()
+
+    def round_mean_weights(self):
+        """The reference's Aggregator.model_weights after the last result of a round (the FedAvg mean,
+        aggregator.py:505-507): fp32 entries float32, int64 entries float64 — materialised lazily."""
+        return LazyWeights(self)
+
+    def _fetch_mean(self) -> list:
+        if not self._mean_valid or self._mean_f is None:
+            raise RuntimeError("the FedAvg mean of this round was not materialised on the device "
+                               "(q-FedAvg discards it; fed-yogi keeps it unless keep_mean=False)")
+        L = self.layout
+        full = self.shards.all_gather(self._mean_f[:L.ld])
+        f_cpu = full[:L.P_full].to("cpu").numpy()
+        s_cpu = self._mean_s[:L.Q].to("cpu").numpy()
+        out = []
+        for e in L.entries:
+            src = f_cpu if e.kind == "f" else s_cpu
+            out.append(np.array(src[e.offset:e.offset + e.numel].reshape(e.shape)))
+        return out
+
+
+class LazyWeights:
+    """List-like stand-in for ``Aggregator.model_weights``: fetched from HBM on first access."""
+
+    def __init__(self, adapter: TorchModelAdapter):
+        self._adapter = adapter
+        self._version = adapter._version
+        self._cache = None
+
+    def _get(self):
+        if self._cache is None:
+            if self._adapter._version != self._version:
+                raise RuntimeError("model_weights of an earlier round: the device buffers were reused")
+            self._cache = self._adapter._fetch_mean()
+        return self._cache
+
+    def __len__(self):
+        return self._adapter.layout.T
+
+    def __getitem__(self, i):
+        return self._get()[i]
+
+    def __iter__(self):
+        return iter(self._get())
+
+    def __deepcopy__(self, memo):
+        import copy
+
+        return copy.deepcopy(self._get(), memo)

@@ -1,0 +1,653 @@
+// fedagg.hip — MI355X (gfx950, CDNA4) kernels for FedScale's aggregator update-reduction path.
+//
+// Everything here is memory-bound streaming arithmetic (~1 flop per 4 B for FedAvg), so the design
+// target is the HBM3E read roofline, not MFMA:
+//   * client updates are client-major [K][ld] fp32; a workgroup owns a contiguous column tile and walks
+//     the client axis in ARRIVAL ORDER, so every element's chain is the reference's sequential
+//     ((u0 + u1) + u2) + ... in fp32 — bit-identical to the numpy loop of aggregator.py:500-503;
+//   * per client, one wave loads V KiB contiguous (16 B/lane dwordx4, non-temporal: every client byte
+//     is read exactly once, so it must not evict anything from L2 / Infinity Cache);
+//   * U clients are loaded before any of them is added (U*V KiB per wave in flight) to cover HBM latency;
+//   * epilogues (÷K, FedYoGi) are fused into the same pass so the global model, m and v make exactly
+//     one round trip; no fused multiply-add anywhere (the reference rounds every op).
+// See DESIGN.md for the roofline arithmetic per kernel.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "../../include/fedagg.h"
+
+#define FA_ABI_VERSION 1
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------
+// error plumbing
+// ------------------------------------------------------------------------------------------------
+static thread_local char g_err[512] = "";
+
+__attribute__((format(printf, 2, 3))) static int fail(int code, const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+  return code;
+}
+static int check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return fail(FA_E_HIP, "%s: launch failed: %s", what, hipGetErrorString(e));
+  return FA_OK;
+}
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+extern "C" int fa_abi_version(void) { return FA_ABI_VERSION; }
+extern "C" const char* fa_last_error_string(void) { return g_err; }
+
+// ------------------------------------------------------------------------------------------------
+// small device helpers
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ f4 ldnt(const f4* p) { return __builtin_nontemporal_load(p); }
+
+__device__ __forceinline__ float sgnf(float x) {  // torch.sign: -1, 0, +1 (NaN passes through)
+  return x > 0.f ? 1.f : (x < 0.f ? -1.f : x);
+}
+__device__ __forceinline__ double sgnd(double x) { return x > 0.0 ? 1.0 : (x < 0.0 ? -1.0 : x); }
+
+// FedYoGi element step, op order of yogi.py:22-31 + optimizers.py:52-58 (fp32, every op rounded).
+__device__ __forceinline__ float yogi_elem(float cur, float last, float& m, float& v, float eta, float tau,
+                                           float beta, float omb, float omb2) {
+  const float g = cur - last;                       // optimizers.py:53  pb - pa
+  const float g2 = g * g;                           // yogi.py:22        gradient**2
+  m = beta * m + omb * g;                           // yogi.py:24
+  v = v - (omb2 * g2) * sgnf(v - g2);               // yogi.py:26-28
+  const float den = __builtin_sqrtf(v) + tau;            // yogi.py:29        sqrt(v) + tau
+  const float lr = __frcp_rn(den) * eta;            //                   eta / t == t.reciprocal() * eta
+  return last + lr * m;                             // yogi.py:31, optimizers.py:58
+}
+
+__device__ __forceinline__ f4 yogi4(f4 cur, f4 last, f4& M, f4& V, float eta, float tau, float beta, float omb,
+                                    float omb2) {
+  float m[4] = {M.x, M.y, M.z, M.w}, v[4] = {V.x, V.y, V.z, V.w};
+  float c[4] = {cur.x, cur.y, cur.z, cur.w}, l[4] = {last.x, last.y, last.z, last.w}, o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = yogi_elem(c[i], l[i], m[i], v[i], eta, tau, beta, omb, omb2);
+  M = f4{m[0], m[1], m[2], m[3]};
+  V = f4{v[0], v[1], v[2], v[3]};
+  return f4{o[0], o[1], o[2], o[3]};
+}
+
+// ------------------------------------------------------------------------------------------------
+// K-way in-order column reduction (+ fused epilogues)
+// ------------------------------------------------------------------------------------------------
+enum { EPI_CHAIN = 0, EPI_MEAN = 1, EPI_YOGI = 2 };
+
+struct RedArgs {
+  const float* x;
+  int64_t ld4;  // row stride in float4
+  int64_t P4;   // float4 columns to produce (ceil(P/4))
+  int K;
+  int flags;
+  const float* a;
+  const float* acc_in;
+  float* out;
+  float denom;
+  const float* last;
+  float* m;
+  float* v;
+  float* mean_out;  // EPI_YOGI: optional copy of chain/denom (the reference's model_weights)
+  float eta, tau, beta, omb, omb2;
+};
+
+// V: float4 per lane per client (a wave covers V KiB contiguous of one client row)
+// U: clients loaded ahead of the adds
+template <int V, int U, int EPI, bool W>
+__global__ __launch_bounds__(256) void k_reduce(RedArgs r) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * (64 * V) + lane;
+  const f4* __restrict__ xp = reinterpret_cast<const f4*>(r.x);
+
+  bool ok[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) ok[j] = (c0 + 64 * j) < r.P4;
+
+  f4 s[V];
+  int k = 0;
+  if (r.flags & FA_ACCUMULATE) {
+    const f4* ain = reinterpret_cast<const f4*>(r.acc_in);
+#pragma unroll
+    for (int j = 0; j < V; ++j) s[j] = ok[j] ? ain[c0 + 64 * j] : f4{0.f, 0.f, 0.f, 0.f};
+  } else {
+    const float w0 = W ? r.a[0] : 1.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      f4 t = ok[j] ? ldnt(xp + c0 + 64 * j) : f4{0.f, 0.f, 0.f, 0.f};
+      s[j] = W ? t * w0 : t;
+    }
+    k = 1;
+  }
+
+  const f4* row = xp + (int64_t)k * r.ld4 + c0;
+  for (; k + U <= r.K; k += U) {
+    f4 t[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+        t[u][j] = ok[j] ? ldnt(row + u * r.ld4 + 64 * j) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float w = W ? r.a[k + u] : 1.f;
+#pragma unroll
+      for (int j = 0; j < V; ++j) s[j] = W ? s[j] + w * t[u][j] : s[j] + t[u][j];
+    }
+    row += U * r.ld4;
+  }
+  for (; k < r.K; ++k) {
+    const float w = W ? r.a[k] : 1.f;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      f4 t = ok[j] ? ldnt(row + 64 * j) : f4{0.f, 0.f, 0.f, 0.f};
+      s[j] = W ? s[j] + w * t : s[j] + t;
+    }
+    row += r.ld4;
+  }
+
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    if (!ok[j]) continue;
+    const int64_t c = c0 + 64 * j;
+    if (EPI == EPI_CHAIN) {
+      reinterpret_cast<f4*>(r.out)[c] = s[j];
+    } else if (EPI == EPI_MEAN) {
+      f4 o;
+      o.x = __fdiv_rn(s[j].x, r.denom);
+      o.y = __fdiv_rn(s[j].y, r.denom);
+      o.z = __fdiv_rn(s[j].z, r.denom);
+      o.w = __fdiv_rn(s[j].w, r.denom);
+      reinterpret_cast<f4*>(r.out)[c] = o;
+    } else {  // EPI_YOGI
+      const f4 L = reinterpret_cast<const f4*>(r.last)[c];
+      f4 M, Vv;
+      if (r.flags & FA_YOGI_INIT) {
+        M = f4{0.f, 0.f, 0.f, 0.f};
+        Vv = f4{r.tau, r.tau, r.tau, r.tau};
+      } else {
+        M = reinterpret_cast<const f4*>(r.m)[c];
+        Vv = reinterpret_cast<const f4*>(r.v)[c];
+      }
+      const f4 cur = f4{__fdiv_rn(s[j].x, r.denom), __fdiv_rn(s[j].y, r.denom), __fdiv_rn(s[j].z, r.denom),
+                        __fdiv_rn(s[j].w, r.denom)};
+      const f4 o = yogi4(cur, L, M, Vv, r.eta, r.tau, r.beta, r.omb, r.omb2);
+      if (r.mean_out) reinterpret_cast<f4*>(r.mean_out)[c] = cur;
+      reinterpret_cast<f4*>(r.m)[c] = M;
+      reinterpret_cast<f4*>(r.v)[c] = Vv;
+      reinterpret_cast<f4*>(r.out)[c] = o;
+    }
+  }
+}
+
+// tuned configuration (see DESIGN.md §kernels / profiles/): V float4 per lane, U clients in flight
+#ifndef FA_RED_V
+#define FA_RED_V 2
+#endif
+#ifndef FA_RED_U
+#define FA_RED_U 8
+#endif
+
+template <int EPI>
+static int launch_reduce(const RedArgs& r, hipStream_t st, const char* what) {
+  constexpr int V = FA_RED_V, U = FA_RED_U;
+  const int64_t per_block = 256LL * V;
+  const int64_t nblk = (r.P4 + per_block - 1) / per_block;
+  if (nblk <= 0) return FA_OK;
+  if (nblk > 0x7fffffffLL) return fail(FA_E_RANGE, "%s: P too large (%lld blocks)", what, (long long)nblk);
+  if (r.a)
+    hipLaunchKernelGGL((k_reduce<V, U, EPI, true>), dim3((unsigned)nblk), dim3(256), 0, st, r);
+  else
+    hipLaunchKernelGGL((k_reduce<V, U, EPI, false>), dim3((unsigned)nblk), dim3(256), 0, st, r);
+  return check_launch(what);
+}
+
+static int check_reduce_args(const char* what, const float* x, int64_t ld, int32_t K, int64_t P,
+                             const float* acc_in, const float* out, int32_t flags) {
+  if (K < 0 || P < 0 || ld < P) return fail(FA_E_ARG, "%s: bad sizes (ld < P or negative)", what);
+  if (ld % 4 != 0) return fail(FA_E_ARG, "%s: ld=%lld must be a multiple of 4", what, (long long)ld);
+  if ((flags & FA_ACCUMULATE) && !acc_in) return fail(FA_E_ARG, "%s: FA_ACCUMULATE without acc_in", what);
+  if (K == 0 && !(flags & FA_ACCUMULATE)) return fail(FA_E_ARG, "%s: K == 0 with nothing to accumulate", what);
+  if (K > 0 && !x) return fail(FA_E_ARG, "%s: x is NULL", what);
+  if (!out) return fail(FA_E_ARG, "%s: out is NULL", what);
+  if (!aligned16(x) || !aligned16(out) || !aligned16(acc_in))
+    return fail(FA_E_ARG, "%s: device pointers must be 16-byte aligned", what);
+  return FA_OK;
+}
+
+extern "C" int fa_reduce(const float* x, int64_t ld, int32_t K, int64_t P, const float* a, const float* acc_in,
+                         float* out, float denom, int32_t flags, fa_stream_t stream) {
+  int e = check_reduce_args("fa_reduce", x, ld, K, P, acc_in, out, flags);
+  if (e) return e;
+  if (P == 0) return FA_OK;
+  RedArgs r{};
+  r.x = x; r.ld4 = ld / 4; r.P4 = (P + 3) / 4; r.K = K; r.flags = flags; r.a = a; r.acc_in = acc_in;
+  r.out = out; r.denom = denom;
+  hipStream_t st = (hipStream_t)stream;
+  if (flags & FA_FINALIZE) return launch_reduce<EPI_MEAN>(r, st, "fa_reduce");
+  return launch_reduce<EPI_CHAIN>(r, st, "fa_reduce");
+}
+
+extern "C" int fa_reduce_yogi(const float* x, int64_t ld, int32_t K, int64_t P, const float* a,
+                              const float* acc_in, float denom, const float* last, float* m, float* v,
+                              float* out, float* mean_out, float eta, float tau, float beta, float omb,
+                              float omb2, int32_t flags, fa_stream_t stream) {
+  int e = check_reduce_args("fa_reduce_yogi", x, ld, K, P, acc_in, out, flags);
+  if (e) return e;
+  if (!last || !m || !v) return fail(FA_E_ARG, "fa_reduce_yogi: last/m/v NULL");
+  if (!aligned16(last) || !aligned16(m) || !aligned16(v) || !aligned16(mean_out))
+    return fail(FA_E_ARG, "fa_reduce_yogi: last/m/v must be 16-byte aligned");
+  if (P == 0) return FA_OK;
+  RedArgs r{};
+  r.x = x; r.ld4 = ld / 4; r.P4 = (P + 3) / 4; r.K = K; r.flags = flags; r.a = a; r.acc_in = acc_in;
+  r.out = out; r.denom = denom; r.last = last; r.m = m; r.v = v; r.mean_out = mean_out;
+  r.eta = eta; r.tau = tau; r.beta = beta; r.omb = omb; r.omb2 = omb2;
+  return launch_reduce<EPI_YOGI>(r, (hipStream_t)stream, "fa_reduce_yogi");
+}
+
+// ------------------------------------------------------------------------------------------------
+// FedYoGi step alone (elementwise, grid-stride float4)
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_yogi_step(const f4* __restrict__ cur, const f4* __restrict__ last,
+                                                   f4* m, f4* v, f4* out, int64_t P4, float eta, float tau,
+                                                   float beta, float omb, float omb2, int init) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P4; i += (int64_t)gridDim.x * 256) {
+    const f4 C = cur[i], L = last[i];
+    f4 M = init ? f4{0.f, 0.f, 0.f, 0.f} : m[i];
+    f4 Vv = init ? f4{tau, tau, tau, tau} : v[i];
+    const f4 o = yogi4(C, L, M, Vv, eta, tau, beta, omb, omb2);
+    m[i] = M;
+    v[i] = Vv;
+    out[i] = o;
+  }
+}
+
+static unsigned stride_grid(int64_t n4) {
+  int64_t b = (n4 + 255) / 256;
+  if (b > 8192) b = 8192;  // 256 CUs x 32 blocks: grid-stride the rest
+  return (unsigned)(b < 1 ? 1 : b);
+}
+
+extern "C" int fa_yogi_step(const float* cur, const float* last, float* m, float* v, float* out, int64_t P,
+                            float eta, float tau, float beta, float omb, float omb2, int32_t flags,
+                            fa_stream_t stream) {
+  if (P < 0) return fail(FA_E_ARG, "fa_yogi_step: negative P");
+  if (P == 0) return FA_OK;
+  if (!cur || !last || !m || !v || !out) return fail(FA_E_ARG, "fa_yogi_step: NULL pointer");
+  if (!aligned16(cur) || !aligned16(last) || !aligned16(m) || !aligned16(v) || !aligned16(out))
+    return fail(FA_E_ARG, "fa_yogi_step: pointers must be 16-byte aligned");
+  const int64_t P4 = (P + 3) / 4;
+  hipLaunchKernelGGL(k_yogi_step, dim3(stride_grid(P4)), dim3(256), 0, (hipStream_t)stream,
+                     (const f4*)cur, (const f4*)last, (f4*)m, (f4*)v, (f4*)out, P4, eta, tau, beta, omb, omb2,
+                     (flags & FA_YOGI_INIT) ? 1 : 0);
+  return check_launch("fa_yogi_step");
+}
+
+// ------------------------------------------------------------------------------------------------
+// q-FedAvg phase 1: delta chain + per-client sum of squares
+// ------------------------------------------------------------------------------------------------
+// Layout: a fixed grid of QF_GRID workgroups (4 waves each) grid-strides over column tiles; the grid
+// size is a constant so the fp64 sum-of-squares order is deterministic across runs and devices.
+// Per tile and client, each lane sums its QF_V*4 squares in fp64, the wave reduces across its 64 lanes
+// (xor butterfly), and lane 0 adds the wave total into an LDS slot [wave][k].  At the end the block
+// writes its 4-wave total per client to workspace[block][k]; k_qfed_gather sums the blocks in order.
+#define QF_V 4
+#define QF_U 2
+#define QF_GRID 1024
+#define QF_MAXK 1024  // LDS: 4 waves x 1024 clients x 8 B = 32 KiB per workgroup
+
+struct QfArgs {
+  const float* x;
+  int64_t ld4, P4;
+  int K;
+  int flags;
+  const float* last;
+  const float* alpha;
+  float lr;
+  float* delta;
+  double* part;  // [gridDim.x][K]
+};
+
+__device__ __forceinline__ double wave_sum(double s) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  return s;
+}
+
+__global__ __launch_bounds__(256) void k_qfed_accum(QfArgs q) {
+  __shared__ double sq[4][QF_MAXK];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  for (int i = threadIdx.x; i < 4 * QF_MAXK; i += 256) (&sq[0][0])[i] = 0.0;
+  __syncthreads();
+
+  const f4* __restrict__ xp = reinterpret_cast<const f4*>(q.x);
+  const int64_t tile_cols = 4LL * 64 * QF_V;
+  const int64_t ntiles = (q.P4 + tile_cols - 1) / tile_cols;
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int64_t c0 = tile * tile_cols + (int64_t)wave * 64 * QF_V + lane;
+    bool ok[QF_V];
+    f4 L[QF_V], D[QF_V];
+#pragma unroll
+    for (int j = 0; j < QF_V; ++j) {
+      ok[j] = (c0 + 64 * j) < q.P4;
+      L[j] = ok[j] ? reinterpret_cast<const f4*>(q.last)[c0 + 64 * j] : f4{0.f, 0.f, 0.f, 0.f};
+      D[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.delta)[c0 + 64 * j]
+                                                  : f4{0.f, 0.f, 0.f, 0.f};
+    }
+    const f4* row = xp + c0;
+    int k = 0;
+    for (; k < q.K; k += QF_U) {
+      f4 t[QF_U][QF_V];
+#pragma unroll
+      for (int u = 0; u < QF_U; ++u)
+#pragma unroll
+        for (int j = 0; j < QF_V; ++j)
+          t[u][j] = (ok[j] && k + u < q.K) ? ldnt(row + (int64_t)u * q.ld4 + 64 * j) : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int u = 0; u < QF_U; ++u) {
+        const int kk = k + u;
+        if (kk >= q.K) break;
+        const float al = q.alpha[kk];
+        const bool first = (kk == 0) && !(q.flags & FA_ACCUMULATE);
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < QF_V; ++j) {
+          f4 g;  // ((last - W) * 1.0) / lr, optimizers.py:82-84 (the *1.0 is exact)
+          g.x = __fdiv_rn(L[j].x - t[u][j].x, q.lr);
+          g.y = __fdiv_rn(L[j].y - t[u][j].y, q.lr);
+          g.z = __fdiv_rn(L[j].z - t[u][j].z, q.lr);
+          g.w = __fdiv_rn(L[j].w - t[u][j].w, q.lr);
+          const f4 term = al * g;  // optimizers.py:89,93  float_power(...) * grad  (fp32 product)
+          D[j] = first ? term : D[j] + term;
+          const f4 g2 = g * g;     // torch.square(grad), fp32
+          acc += (double)g2.x;
+          acc += (double)g2.y;
+          acc += (double)g2.z;
+          acc += (double)g2.w;
+        }
+        acc = wave_sum(acc);
+        if (lane == 0) sq[wave][kk] += acc;
+      }
+      row += QF_U * q.ld4;
+    }
+#pragma unroll
+    for (int j = 0; j < QF_V; ++j)
+      if (ok[j]) reinterpret_cast<f4*>(q.delta)[c0 + 64 * j] = D[j];
+  }
+  __syncthreads();
+  for (int k = threadIdx.x; k < q.K; k += 256)
+    q.part[(int64_t)blockIdx.x * q.K + k] = ((sq[0][k] + sq[1][k]) + sq[2][k]) + sq[3][k];
+}
+
+__global__ __launch_bounds__(256) void k_qfed_gather(const double* __restrict__ part, int nblk, int K,
+                                                     double* sqnorm) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b) s += part[(int64_t)b * K + k];
+  sqnorm[k] += s;
+}
+
+extern "C" int fa_qfed_max_chunk(void) { return QF_MAXK; }
+extern "C" int64_t fa_qfed_workspace_bytes(int32_t K) { return (int64_t)QF_GRID * (K > 0 ? K : 1) * 8; }
+
+extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t P, const float* last,
+                                  const float* alpha, float lr, float* delta, double* sqnorm, void* workspace,
+                                  int32_t flags, fa_stream_t stream) {
+  if (K <= 0 || K > QF_MAXK) return fail(FA_E_RANGE, "fa_qfed_accumulate: K=%d outside [1, %d]", (int)K, QF_MAXK);
+  if (P < 0 || ld < P || ld % 4) return fail(FA_E_ARG, "fa_qfed_accumulate: bad P/ld");
+  if (!x || !last || !alpha || !delta || !sqnorm || !workspace)
+    return fail(FA_E_ARG, "fa_qfed_accumulate: NULL pointer");
+  if (!aligned16(x) || !aligned16(last) || !aligned16(delta))
+    return fail(FA_E_ARG, "fa_qfed_accumulate: x/last/delta must be 16-byte aligned");
+  QfArgs q{};
+  q.x = x; q.ld4 = ld / 4; q.P4 = (P + 3) / 4; q.K = K; q.flags = flags; q.last = last; q.alpha = alpha;
+  q.lr = lr; q.delta = delta; q.part = (double*)workspace;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_qfed_accum, dim3(QF_GRID), dim3(256), 0, st, q);
+  int e = check_launch("fa_qfed_accumulate");
+  if (e) return e;
+  hipLaunchKernelGGL(k_qfed_gather, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)workspace,
+                     (int)QF_GRID, (int)K, sqnorm);
+  return check_launch("fa_qfed_accumulate(gather)");
+}
+
+__global__ void k_qfed_hs(const double* sqnorm, const float* c1, const float* c2, int K, float* hs_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float hs = 0.f;  // optimizers.py:70  hs = 0.0; first `0.0 + t` is exact
+  for (int k = 0; k < K; ++k) {
+    const float s = (float)sqnorm[k];      // torch.sum(...) of fp32 -> fp32
+    const float t = c1[k] * s + c2[k];     // (q*a^(q-1)) * S + (1/lr)*a^q   — two fp32 roundings, no FMA
+    hs = hs + t;
+  }
+  hs_out[0] = hs;
+  hs_out[1] = hs + 1e-10f;                 // optimizers.py:102 (hs + 1e-10)
+}
+
+extern "C" int fa_qfed_hs(const double* sqnorm, const float* c1, const float* c2, int32_t K, float* hs_out,
+                          fa_stream_t stream) {
+  if (K < 0 || !sqnorm || !c1 || !c2 || !hs_out) return fail(FA_E_ARG, "fa_qfed_hs: bad arguments");
+  hipLaunchKernelGGL(k_qfed_hs, dim3(1), dim3(64), 0, (hipStream_t)stream, sqnorm, c1, c2, (int)K, hs_out);
+  return check_launch("fa_qfed_hs");
+}
+
+__global__ __launch_bounds__(256) void k_qfed_finalize(const f4* __restrict__ last, const f4* __restrict__ delta,
+                                                       const float* __restrict__ hs, f4* out, int64_t P4) {
+  const float d = hs[1];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P4; i += (int64_t)gridDim.x * 256) {
+    const f4 L = last[i], D = delta[i];
+    f4 o;
+    o.x = L.x - __fdiv_rn(D.x, d);
+    o.y = L.y - __fdiv_rn(D.y, d);
+    o.z = L.z - __fdiv_rn(D.z, d);
+    o.w = L.w - __fdiv_rn(D.w, d);
+    out[i] = o;
+  }
+}
+
+extern "C" int fa_qfed_finalize(const float* last, const float* delta, const float* hs_dev, float* out, int64_t P,
+                                fa_stream_t stream) {
+  if (P < 0 || !last || !delta || !hs_dev || !out) return fail(FA_E_ARG, "fa_qfed_finalize: bad arguments");
+  if (!aligned16(last) || !aligned16(delta) || !aligned16(out))
+    return fail(FA_E_ARG, "fa_qfed_finalize: pointers must be 16-byte aligned");
+  if (P == 0) return FA_OK;
+  const int64_t P4 = (P + 3) / 4;
+  hipLaunchKernelGGL(k_qfed_finalize, dim3(stride_grid(P4)), dim3(256), 0, (hipStream_t)stream,
+                     (const f4*)last, (const f4*)delta, hs_dev, (f4*)out, P4);
+  return check_launch("fa_qfed_finalize");
+}
+
+// ------------------------------------------------------------------------------------------------
+// side table (int64 state_dict entries): one thread per element, clients in arrival order
+// ------------------------------------------------------------------------------------------------
+__global__ void k_side_accum(const int64_t* xi, int ldq, int K, int Q, int mode, const double* w, int64_t* acc_i,
+                             double* acc_d, int accumulate) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  if (mode == 0) {
+    int64_t s = accumulate ? acc_i[q] : xi[q];
+    for (int k = accumulate ? 0 : 1; k < K; ++k)
+      s = (int64_t)((uint64_t)s + (uint64_t)xi[(int64_t)k * ldq + q]);  // numpy int64 add wraps
+    acc_i[q] = s;
+  } else {
+    double s = accumulate ? acc_d[q] : (double)xi[q] * w[0];
+    for (int k = accumulate ? 0 : 1; k < K; ++k) s = s + w[k] * (double)xi[(int64_t)k * ldq + q];
+    acc_d[q] = s;
+  }
+}
+
+extern "C" int fa_side_accumulate(const int64_t* xi, int32_t ldq, int32_t K, int32_t Q, int32_t mode,
+                                  const double* w, int64_t* acc_i, double* acc_d, int32_t flags,
+                                  fa_stream_t stream) {
+  if (Q == 0) return FA_OK;
+  if (Q < 0 || K < 0 || ldq < Q || (K > 0 && !xi)) return fail(FA_E_ARG, "fa_side_accumulate: bad sizes");
+  if (mode == 0 && !acc_i) return fail(FA_E_ARG, "fa_side_accumulate: acc_i NULL");
+  if (mode == 1 && (!acc_d || !w)) return fail(FA_E_ARG, "fa_side_accumulate: acc_d/w NULL");
+  if (mode != 0 && mode != 1) return fail(FA_E_ARG, "fa_side_accumulate: mode %d", (int)mode);
+  if (K == 0) return FA_OK;
+  hipLaunchKernelGGL(k_side_accum, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, xi, ldq, K, Q, mode, w,
+                     acc_i, acc_d, (flags & FA_ACCUMULATE) ? 1 : 0);
+  return check_launch("fa_side_accumulate");
+}
+
+__global__ void k_side_close(const int64_t* acc_i, const double* acc_d, int Q, int mode, double denom, double* cur,
+                             int64_t* model) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  const double c = (mode == 0 ? (double)acc_i[q] : acc_d[q]) / denom;
+  if (cur) cur[q] = c;
+  if (model) model[q] = (int64_t)(float)c;  // np.asarray(float32) then float32 -> int64 copy (truncation)
+}
+
+extern "C" int fa_side_close(const int64_t* acc_i, const double* acc_d, int32_t Q, int32_t mode, double denom,
+                             double* cur, int64_t* model, fa_stream_t stream) {
+  if (Q == 0) return FA_OK;
+  if (Q < 0 || (mode == 0 && !acc_i) || (mode == 1 && !acc_d)) return fail(FA_E_ARG, "fa_side_close: bad args");
+  hipLaunchKernelGGL(k_side_close, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, acc_i, acc_d, Q, mode,
+                     denom, cur, model);
+  return check_launch("fa_side_close");
+}
+
+__global__ void k_side_yogi(const double* cur, const int64_t* last, double* m, double* v, double* step,
+                            int64_t* model, int Q, double eta, double tau, double beta, double omb, double omb2,
+                            int init) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  const double L = last ? (double)last[q] : 0.0;
+  const double g = cur[q] - L;
+  const double g2 = g * g;
+  double M = init ? 0.0 : m[q];
+  double Vv = init ? tau : v[q];
+  M = beta * M + omb * g;
+  Vv = Vv - (omb2 * g2) * sgnd(Vv - g2);
+  const double lr = __drcp_rn(__builtin_sqrt(Vv) + tau) * eta;
+  const double st = lr * M;
+  m[q] = M;
+  v[q] = Vv;
+  if (step) step[q] = st;
+  if (model) model[q] = (int64_t)(float)(L + st);  // np.array(last + diff, float32) -> load_state_dict
+}
+
+extern "C" int fa_side_yogi(const double* cur, const int64_t* last, double* m, double* v, double* step,
+                            int64_t* model, int32_t Q, double eta, double tau, double beta, double omb, double omb2,
+                            int32_t flags, fa_stream_t stream) {
+  if (Q == 0) return FA_OK;
+  if (Q < 0 || !cur || !m || !v) return fail(FA_E_ARG, "fa_side_yogi: bad args");
+  hipLaunchKernelGGL(k_side_yogi, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, cur, last, m, v, step,
+                     model, Q, eta, tau, beta, omb, omb2, (flags & FA_YOGI_INIT) ? 1 : 0);
+  return check_launch("fa_side_yogi");
+}
+
+// q-FedAvg side: (a) one thread per element walks the clients (delta chain);
+//                (b) one thread per client walks the elements (sum of g^2 in element order).
+__device__ __forceinline__ float side_g(int64_t L, int64_t W, float lr) {
+  // (u - v) int64, then "* 1.0" promotes to fp32 (int64 -> fp32 conversion, times 1.0f), then / lr
+  return __fdiv_rn((float)(int64_t)((uint64_t)L - (uint64_t)W) * 1.0f, lr);
+}
+
+__global__ void k_side_qfed_delta(const int64_t* xi, int ldq, int K, int Q, const int64_t* last, const float* alpha,
+                                  float lr, float* delta_s, int accumulate) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  float d = accumulate ? delta_s[q] : 0.f;
+  for (int k = 0; k < K; ++k) {
+    const float t = alpha[k] * side_g(last[q], xi[(int64_t)k * ldq + q], lr);
+    d = (k == 0 && !accumulate) ? t : d + t;
+  }
+  delta_s[q] = d;
+}
+
+__global__ void k_side_qfed_sq(const int64_t* xi, int ldq, int K, int Q, const int64_t* last, float lr,
+                               double* sqnorm) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  double s = 0.0;
+  for (int q = 0; q < Q; ++q) {
+    const float g = side_g(last[q], xi[(int64_t)k * ldq + q], lr);
+    s += (double)(g * g);
+  }
+  sqnorm[k] += s;
+}
+
+extern "C" int fa_side_qfed_accumulate(const int64_t* xi, int32_t ldq, int32_t K, int32_t Q, const int64_t* last,
+                                       const float* alpha, float lr, float* delta_s, double* sqnorm, int32_t flags,
+                                       fa_stream_t stream) {
+  if (Q == 0 || K == 0) return FA_OK;
+  if (Q < 0 || K < 0 || ldq < Q || !xi || !last || !alpha || !delta_s || !sqnorm)
+    return fail(FA_E_ARG, "fa_side_qfed_accumulate: bad args");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_side_qfed_delta, dim3((Q + 63) / 64), dim3(64), 0, st, xi, ldq, K, Q, last, alpha, lr, delta_s,
+                     (flags & FA_ACCUMULATE) ? 1 : 0);
+  int e = check_launch("fa_side_qfed_accumulate(delta)");
+  if (e) return e;
+  hipLaunchKernelGGL(k_side_qfed_sq, dim3((K + 63) / 64), dim3(64), 0, st, xi, ldq, K, Q, last, lr, sqnorm);
+  return check_launch("fa_side_qfed_accumulate(sq)");
+}
+
+__global__ void k_side_qfed_finalize(const int64_t* last, const float* delta_s, const float* hs, int64_t* model,
+                                     int Q) {
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= Q) return;
+  model[q] = (int64_t)((float)last[q] - __fdiv_rn(delta_s[q], hs[1]));
+}
+
+extern "C" int fa_side_qfed_finalize(const int64_t* last, const float* delta_s, const float* hs_dev, int64_t* model,
+                                     int32_t Q, fa_stream_t stream) {
+  if (Q == 0) return FA_OK;
+  if (Q < 0 || !last || !delta_s || !hs_dev || !model) return fail(FA_E_ARG, "fa_side_qfed_finalize: bad args");
+  hipLaunchKernelGGL(k_side_qfed_finalize, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, last, delta_s,
+                     hs_dev, model, Q);
+  return check_launch("fa_side_qfed_finalize");
+}
+
+// ------------------------------------------------------------------------------------------------
+// deterministic synthetic updates (bit-reproducible on the host: fedscale_amd/synth.py)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ float tri(uint32_t stream, int64_t p) {
+  const uint32_t h = mix32(mix32((uint32_t)p + mix32(stream)) ^ (uint32_t)((uint64_t)p >> 32));
+  const int32_t u1 = (int32_t)(h >> 8), u2 = (int32_t)(mix32(h) >> 8);
+  return (float)(u1 + u2 - (1 << 24)) * 5.9604644775390625e-08f;  // exact: |n| <= 2^24, times 2^-24
+}
+
+__global__ __launch_bounds__(256) void k_fill(float* x, int64_t ld, int K, int64_t P, uint32_t seed, int k0,
+                                              float sb, float sn) {
+  const int k = blockIdx.y;
+  float* row = x + (int64_t)k * ld;
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < ld; p += (int64_t)gridDim.x * 256) {
+    float val = 0.f;
+    if (p < P) {
+      const float b = tri(seed, p) * sb;
+      const float n = tri(seed + 1u + (uint32_t)(k0 + k), p) * sn;
+      val = b + n;
+    }
+    row[p] = val;
+  }
+}
+
+extern "C" int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uint32_t seed, int32_t k0,
+                                 float scale_base, float scale_noise, fa_stream_t stream) {
+  if (K < 0 || P < 0 || ld < P || !x) return fail(FA_E_ARG, "fa_fill_synthetic: bad args");
+  if (K == 0 || ld == 0) return FA_OK;
+  if (K > 65535) return fail(FA_E_RANGE, "fa_fill_synthetic: K=%d > 65535 per call", (int)K);
+  int64_t gx = (ld + 255) / 256;
+  if (gx > 2048) gx = 2048;
+  hipLaunchKernelGGL(k_fill, dim3((unsigned)gx, (unsigned)K), dim3(256), 0, (hipStream_t)stream, x, ld, K, P, seed, k0,
+                     scale_base, scale_noise);
+  return check_launch("fa_fill_synthetic");
+}

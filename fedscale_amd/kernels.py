@@ -1,0 +1,180 @@
+"""Typed torch-tensor wrappers over the C ABI (include/fedagg.h).
+
+Each wrapper validates device / dtype / contiguity / size on the host (stricter than the reference,
+identical on valid input) and launches on the current HIP stream of the tensor's device.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import _native as N
+from ._native import FA_ACCUMULATE, FA_FINALIZE, FA_YOGI_INIT, call, ptr
+
+
+def _dev(t: torch.Tensor, dtype, name: str, min_numel: int = 0, align: int = 16):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor, got {type(t).__name__}")
+    if t.device.type != "cuda":
+        raise ValueError(f"{name}: must be a device tensor (got {t.device}); the HIP path has no CPU fallback")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if t.numel() < min_numel:
+        raise ValueError(f"{name}: has {t.numel()} elements, needs >= {min_numel}")
+    if t.data_ptr() % align:
+        raise ValueError(f"{name}: device pointer must be {align}-byte aligned")
+
+
+def _cols(P: int) -> int:
+    return (P + 3) // 4 * 4
+
+
+def _stream(t: torch.Tensor):
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def _check_x(x: torch.Tensor, K: int, P: int):
+    _dev(x, torch.float32, "x")
+    if x.dim() != 2:
+        raise ValueError("x: expected a [K, ld] client-major buffer")
+    if K > x.shape[0]:
+        raise ValueError(f"x: K={K} > rows {x.shape[0]}")
+    ld = x.shape[1]
+    if ld < P or ld % 4:
+        raise ValueError(f"x: ld={ld} must be >= P={P} and a multiple of 4")
+    return ld
+
+
+def reduce(x: torch.Tensor, K: int, P: int, out: torch.Tensor, *, a: Optional[torch.Tensor] = None,
+           acc_in: Optional[torch.Tensor] = None, denom: float = 1.0, finalize: bool = False) -> torch.Tensor:
+    """In-order weighted column reduction of x[:K, :P] (fa_reduce)."""
+    ld = _check_x(x, K, P) if K > 0 else (x.shape[1] if x is not None else _cols(P))
+    _dev(out, torch.float32, "out", _cols(P))
+    if a is not None:
+        _dev(a, torch.float32, "a", K, align=4)
+    if acc_in is not None:
+        _dev(acc_in, torch.float32, "acc_in", _cols(P))
+    flags = (FA_ACCUMULATE if acc_in is not None else 0) | (FA_FINALIZE if finalize else 0)
+    call("fa_reduce", ptr(x) if K > 0 else None, ld, K, P, ptr(a), ptr(acc_in), ptr(out), float(denom), flags,
+         _stream(out))
+    return out
+
+
+def reduce_yogi(x, K, P, *, last, m, v, out, denom, eta, tau, beta, omb, omb2, init, a=None, acc_in=None,
+                mean_out=None):
+    ld = _check_x(x, K, P) if K > 0 else x.shape[1]
+    for n, t in (("last", last), ("m", m), ("v", v), ("out", out)):
+        _dev(t, torch.float32, n, _cols(P))
+    if a is not None:
+        _dev(a, torch.float32, "a", K, align=4)
+    if acc_in is not None:
+        _dev(acc_in, torch.float32, "acc_in", _cols(P))
+    if mean_out is not None:
+        _dev(mean_out, torch.float32, "mean_out", _cols(P))
+    flags = (FA_ACCUMULATE if acc_in is not None else 0) | FA_FINALIZE | (FA_YOGI_INIT if init else 0)
+    call("fa_reduce_yogi", ptr(x) if K > 0 else None, ld, K, P, ptr(a), ptr(acc_in), float(denom), ptr(last),
+         ptr(m), ptr(v), ptr(out), ptr(mean_out), float(eta), float(tau), float(beta), float(omb), float(omb2), flags,
+         _stream(out))
+    return out
+
+
+def yogi_step(cur, last, m, v, out, P, *, eta, tau, beta, omb, omb2, init):
+    for n, t in (("cur", cur), ("last", last), ("m", m), ("v", v), ("out", out)):
+        _dev(t, torch.float32, n, _cols(P))
+    call("fa_yogi_step", ptr(cur), ptr(last), ptr(m), ptr(v), ptr(out), P, float(eta), float(tau), float(beta),
+         float(omb), float(omb2), FA_YOGI_INIT if init else 0, _stream(out))
+    return out
+
+
+def qfed_max_chunk() -> int:
+    return N.load().fa_qfed_max_chunk()
+
+
+def qfed_workspace(K: int, device) -> torch.Tensor:
+    nbytes = N.load().fa_qfed_workspace_bytes(K)
+    return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
+
+
+def qfed_accumulate(x, K, P, *, last, alpha, lr, delta, sqnorm, workspace, accumulate):
+    ld = _check_x(x, K, P)
+    _dev(last, torch.float32, "last", _cols(P))
+    _dev(delta, torch.float32, "delta", _cols(P))
+    _dev(alpha, torch.float32, "alpha", K, align=4)
+    _dev(sqnorm, torch.float64, "sqnorm", K, align=8)
+    _dev(workspace, torch.float64, "workspace")
+    if workspace.numel() * 8 < N.load().fa_qfed_workspace_bytes(K):
+        raise ValueError("workspace too small")
+    call("fa_qfed_accumulate", ptr(x), ld, K, P, ptr(last), ptr(alpha), float(lr), ptr(delta), ptr(sqnorm),
+         ptr(workspace), FA_ACCUMULATE if accumulate else 0, _stream(delta))
+
+
+def qfed_hs(sqnorm, c1, c2, K, hs_out):
+    _dev(sqnorm, torch.float64, "sqnorm", K, align=8)
+    _dev(c1, torch.float32, "c1", K, align=4)
+    _dev(c2, torch.float32, "c2", K, align=4)
+    _dev(hs_out, torch.float32, "hs_out", 2)
+    call("fa_qfed_hs", ptr(sqnorm), ptr(c1), ptr(c2), K, ptr(hs_out), _stream(hs_out))
+
+
+def qfed_finalize(last, delta, hs, out, P):
+    for n, t in (("last", last), ("delta", delta), ("out", out)):
+        _dev(t, torch.float32, n, _cols(P))
+    _dev(hs, torch.float32, "hs", 2)
+    call("fa_qfed_finalize", ptr(last), ptr(delta), ptr(hs), ptr(out), P, _stream(out))
+
+
+# ---- side table (int64 entries) ---------------------------------------------------------------
+def side_accumulate(xi, K, Q, mode, *, w=None, acc_i=None, acc_d=None, accumulate=False):
+    if Q == 0 or K == 0:
+        return
+    _dev(xi, torch.int64, "xi", align=8)
+    ldq = xi.shape[1]
+    if mode == 0:
+        _dev(acc_i, torch.int64, "acc_i", Q, align=8)
+    else:
+        _dev(acc_d, torch.float64, "acc_d", Q, align=8)
+        _dev(w, torch.float64, "w", K, align=8)
+    call("fa_side_accumulate", ptr(xi), ldq, K, Q, mode, ptr(w), ptr(acc_i), ptr(acc_d),
+         FA_ACCUMULATE if accumulate else 0, _stream(xi))
+
+
+def side_close(Q, mode, denom, *, acc_i=None, acc_d=None, cur=None, model=None):
+    if Q == 0:
+        return
+    ref = acc_i if mode == 0 else acc_d
+    call("fa_side_close", ptr(acc_i), ptr(acc_d), Q, mode, float(denom), ptr(cur), ptr(model), _stream(ref))
+
+
+def side_yogi(cur, last, m, v, Q, *, step=None, model=None, eta, tau, beta, omb, omb2, init):
+    if Q == 0:
+        return
+    call("fa_side_yogi", ptr(cur), ptr(last), ptr(m), ptr(v), ptr(step), ptr(model), Q, float(eta), float(tau), float(beta),
+         float(omb), float(omb2), FA_YOGI_INIT if init else 0, _stream(cur))
+
+
+def side_qfed_accumulate(xi, K, Q, *, last, alpha, lr, delta_s, sqnorm, accumulate):
+    if Q == 0 or K == 0:
+        return
+    _dev(xi, torch.int64, "xi", align=8)
+    call("fa_side_qfed_accumulate", ptr(xi), xi.shape[1], K, Q, ptr(last), ptr(alpha), float(lr), ptr(delta_s),
+         ptr(sqnorm), FA_ACCUMULATE if accumulate else 0, _stream(xi))
+
+
+def side_qfed_finalize(last, delta_s, hs, model, Q):
+    if Q == 0:
+        return
+    call("fa_side_qfed_finalize", ptr(last), ptr(delta_s), ptr(hs), ptr(model), Q, _stream(model))
+
+
+def fill_synthetic(x: torch.Tensor, K: int, P: int, *, seed: int, k0: int = 0, scale_base: float = 0.05,
+                   scale_noise: float = 0.01):
+    _dev(x, torch.float32, "x")
+    ld = x.shape[1]
+    if K > x.shape[0] or ld < P:
+        raise ValueError("fill_synthetic: x too small")
+    call("fa_fill_synthetic", ptr(x), ld, K, P, seed & 0xFFFFFFFF, k0, float(scale_base), float(scale_noise),
+         _stream(x))
+    return x

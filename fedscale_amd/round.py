@@ -1,0 +1,184 @@
+"""One aggregation round on the device: staging of arriving client updates + chunked in-order reduction.
+
+A ``DeviceRound`` is the device-side state that replaces the reference's ``self.model_weights`` running
+sum (aggregator.py:497-503 / async_aggregator.py:129-133) and, for q-FedAvg, its retained
+``client_training_results`` (aggregator.py:466-467, consumed by optimizers.py:73-98).  Updates are
+staged into a [capacity, ld] device buffer; whenever it fills before the round ends, the chunk is
+folded into the running state by one kernel launch (the same per-element chain continues, so chunking
+never changes a bit of the result).  The last chunk is reduced by ``finalize_*`` with the server step
+fused in.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import kernels as kx
+from .bucket import BucketLayout, ClientStaging
+
+POLICIES = ("fedavg", "fedbuff", "qfedavg")
+
+
+def default_capacity(layout: BucketLayout, K: int, device, budget_fraction: float = 0.5,
+                     hard_cap: Optional[int] = None) -> int:
+    """Clients per chunk: all K when they fit in ``budget_fraction`` of the free HBM."""
+    free, _ = torch.cuda.mem_get_info(device)
+    per_client = layout.ld * 4 + layout.ldq * 8
+    cap = max(1, int(free * budget_fraction) // max(1, per_client))
+    cap = min(cap, max(1, K))
+    if hard_cap:
+        cap = min(cap, hard_cap)
+    return cap
+
+
+class DeviceRound:
+    def __init__(self, layout: BucketLayout, device, K: int, policy: str, *, capacity: Optional[int] = None,
+                 staging: Optional[ClientStaging] = None, last_f32: Optional[torch.Tensor] = None,
+                 last_i64: Optional[torch.Tensor] = None):
+        if policy not in POLICIES:
+            raise ValueError(f"policy {policy!r} not in {POLICIES}")
+        if K < 1:
+            raise ValueError("a round needs K >= 1 client results")
+        self.layout, self.device, self.K, self.policy = layout, torch.device(device), int(K), policy
+        if policy == "qfedavg":
+            qmax = kx.qfed_max_chunk()
+            capacity = min(capacity or qmax, qmax)
+        if staging is not None and (capacity is None or staging.capacity >= min(capacity, K)):
+            self.staging = staging
+        else:
+            cap = capacity or default_capacity(layout, K, self.device)
+            self.staging = ClientStaging(layout, self.device, min(cap, K))
+        self.cap = min(self.staging.capacity, capacity or self.staging.capacity)
+        self.n = 0  # results received
+        self.slot = 0  # staged in the current chunk
+        self.chunks_done = 0
+        dev, L = self.device, layout
+        self.acc = None  # running fp32 chain across chunks
+        self.acc_i = torch.zeros(L.ldq, dtype=torch.int64, device=dev)
+        self.acc_d = torch.zeros(L.ldq, dtype=torch.float64, device=dev)
+        self._w32 = np.zeros(self.cap, dtype=np.float32)  # per-slot weights of the current chunk
+        self._w64 = np.zeros(self.cap, dtype=np.float64)
+        self.last_f32, self.last_i64 = last_f32, last_i64
+        if policy == "qfedavg":
+            if last_f32 is None or last_i64 is None:
+                raise ValueError("q-FedAvg needs the round's starting model (last_f32 / last_i64)")
+            self.delta = torch.zeros(L.ld, dtype=torch.float32, device=dev)
+            self.delta_s = torch.zeros(L.ldq, dtype=torch.float32, device=dev)
+            self.sqnorm = torch.zeros(self.K, dtype=torch.float64, device=dev)       # fp32 bucket part (per shard)
+            self.sqnorm_side = torch.zeros(self.K, dtype=torch.float64, device=dev)  # side table part (replicated)
+            self.workspace = kx.qfed_workspace(self.cap, dev)
+            self.alpha = np.zeros(self.K, dtype=np.float32)
+            self.c1 = np.zeros(self.K, dtype=np.float32)
+            self.c2 = np.zeros(self.K, dtype=np.float32)
+            self.lr = None
+
+    # ---------------------------------------------------------------------------------------------
+    def add(self, update, *, weight: Optional[float] = None, loss: Optional[float] = None,
+            learning_rate: Optional[float] = None, q: Optional[float] = None):
+        """Stage one arriving client update (in arrival order)."""
+        if self.n >= self.K:
+            raise RuntimeError(f"round already has its K={self.K} results")
+        if self.slot == self.cap:
+            self._fold_chunk()
+        self.staging.put(self.slot, update)
+        if self.policy == "fedbuff":
+            self._w32[self.slot] = np.float32(weight)  # fp32 array * Python float: scalar rounds to fp32
+            self._w64[self.slot] = float(weight)       # int64 array * Python float: float64
+        elif self.policy == "qfedavg":
+            self._qfed_scalars(self.n, loss, learning_rate, q)
+        self.slot += 1
+        self.n += 1
+
+    def _qfed_scalars(self, k, loss, lr, q):
+        """Per-client scalars of optimizers.py:87-98, computed in double exactly as the reference does."""
+        base = loss + 1e-10
+        a = np.float_power(base, q)
+        self.alpha[k] = np.float32(a)                         # a * grad: scalar rounded to fp32
+        self.c1[k] = np.float32(q * np.float_power(base, q - 1))
+        self.c2[k] = np.float32((1.0 / lr) * a)
+        if self.lr is None:
+            self.lr = lr
+        elif lr != self.lr:
+            raise RuntimeError("learning_rate changed in the middle of a q-FedAvg round")
+
+    def _chunk_weights(self):
+        n = self.slot
+        a32 = torch.from_numpy(self._w32[:n].copy()).to(self.device, non_blocking=True)
+        a64 = torch.from_numpy(self._w64[:n].copy()).to(self.device, non_blocking=True)
+        return a32, a64
+
+    def _fold_chunk(self):
+        """Fold the staged chunk into the running state (not the last chunk of the round)."""
+        L, st, n = self.layout, self.staging, self.slot
+        first = self.chunks_done == 0
+        if self.policy in ("fedavg", "fedbuff"):
+            if self.acc is None:
+                self.acc = torch.zeros(L.ld, dtype=torch.float32, device=self.device)
+            a32 = a64 = None
+            if self.policy == "fedbuff":
+                a32, a64 = self._chunk_weights()
+            kx.reduce(st.x, n, L.P, self.acc, a=a32, acc_in=None if first else self.acc)
+            kx.side_accumulate(st.xi, n, L.Q, 0 if self.policy == "fedavg" else 1, w=a64, acc_i=self.acc_i,
+                               acc_d=self.acc_d, accumulate=not first)
+        else:
+            k0 = self.n - n
+            alpha = torch.from_numpy(self.alpha[k0:k0 + n].copy()).to(self.device, non_blocking=True)
+            if L.P > 0:
+                kx.qfed_accumulate(st.x, n, L.P, last=self.last_f32, alpha=alpha, lr=self.lr, delta=self.delta,
+                                   sqnorm=self.sqnorm[k0:k0 + n], workspace=self.workspace, accumulate=not first)
+            kx.side_qfed_accumulate(st.xi, n, L.Q, last=self.last_i64, alpha=alpha, lr=self.lr,
+                                    delta_s=self.delta_s, sqnorm=self.sqnorm_side[k0:k0 + n], accumulate=not first)
+        self.chunks_done += 1
+        self.slot = 0
+
+    def _check_complete(self):
+        if self.n != self.K:
+            raise RuntimeError(f"finalize with {self.n} of K={self.K} results")
+
+    # ---- FedAvg / FedBuff: mean (+ optional fused FedYoGi) --------------------------------------
+    def finalize_mean(self, denom32: float, denom64: float, *, out: torch.Tensor, cur_side: torch.Tensor,
+                      model_side: Optional[torch.Tensor] = None, yogi: Optional[dict] = None):
+        """Reduce the last chunk with the epilogue fused.
+
+        out        <- fp32 mean (or, with ``yogi``, the new global model last + step)
+        cur_side   <- float64 mean of the side table (np.divide of int64 sums)
+        model_side <- int64(fp32(mean)) (what load_state_dict stores), when given
+        yogi       -> dict(last=, m=, v=, eta=, tau=, beta=, omb=, omb2=, init=)
+        """
+        self._check_complete()
+        L, st, n = self.layout, self.staging, self.slot
+        first = self.chunks_done == 0
+        a32 = a64 = None
+        if self.policy == "fedbuff":
+            a32, a64 = self._chunk_weights()
+        acc_in = None if first else self.acc
+        if yogi is None:
+            kx.reduce(st.x, n, L.P, out, a=a32, acc_in=acc_in, denom=denom32, finalize=True)
+        else:
+            kx.reduce_yogi(st.x, n, L.P, a=a32, acc_in=acc_in, denom=denom32, out=out, **yogi)
+        mode = 0 if self.policy == "fedavg" else 1
+        kx.side_accumulate(st.xi, n, L.Q, mode, w=a64, acc_i=self.acc_i, acc_d=self.acc_d, accumulate=not first)
+        kx.side_close(L.Q, mode, denom64, acc_i=self.acc_i, acc_d=self.acc_d, cur=cur_side, model=model_side)
+
+    # ---- q-FedAvg --------------------------------------------------------------------------------
+    def finalize_qfed(self, *, out: torch.Tensor, model_side: torch.Tensor, sqnorm_allreduce=None):
+        """Fold the last chunk, then hs (optimizers.py:96-98) and new = L - delta/(hs+1e-10) (:101-104).
+
+        ``sqnorm_allreduce(t)`` sums the per-client partial squared norms across shards (RCCL) when the
+        model is sharded over ranks; the side table contributes once, after the all-reduce."""
+        self._check_complete()
+        L = self.layout
+        if self.slot:
+            self._fold_chunk()
+        if sqnorm_allreduce is not None:
+            sqnorm_allreduce(self.sqnorm)
+        # side table: replicated on every rank, so it is added once, after the cross-shard sum
+        self.sqnorm += self.sqnorm_side
+        c1 = torch.from_numpy(self.c1).to(self.device, non_blocking=True)
+        c2 = torch.from_numpy(self.c2).to(self.device, non_blocking=True)
+        self.hs = torch.zeros(2, dtype=torch.float32, device=self.device)
+        kx.qfed_hs(self.sqnorm, c1, c2, self.K, self.hs)
+        kx.qfed_finalize(self.last_f32, self.delta, self.hs, out, L.P)
+        kx.side_qfed_finalize(self.last_i64, self.delta_s, self.hs, model_side, L.Q)

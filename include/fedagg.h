@@ -1,0 +1,152 @@
+/*
+ * fedagg.h — C ABI of the MI355X (gfx950) aggregator update-reduction path.
+ *
+ * This library replaces the arithmetic of FedScale's aggregator hot path (FedScale v0.5,
+ * /root/reference).  The reference has no native code and no FFI on this path: its "interface" is the
+ * Python plugin surface listed per entry point below, and the binding a maintainer adds is the ctypes
+ * layer in fedscale_amd/_native.py (INTEGRATION.md shows it).
+ *
+ * Conventions (all entry points):
+ *   - return 0 on success, a negative FA_E* code on failure; fa_last_error_string() describes the
+ *     last failure of the calling thread.  No exception crosses the ABI.
+ *   - every pointer is DEVICE memory owned by the caller (16-byte aligned); every launch is
+ *     asynchronous on the caller's `stream` (a hipStream_t; NULL = the legacy default stream) with no
+ *     implicit synchronisation.  Functions are stateless and reentrant.
+ *   - a "bucket" is the fp32 tensors of a state_dict concatenated in state_dict order: P elements,
+ *     padded with zeros to a row stride `ld` (multiple of 64).  Client updates live client-major,
+ *     x[k*ld + p].  Every per-column buffer (acc, out, last, m, v, delta) holds >= round_up(P, 4)
+ *     elements.  Non-fp32 (int64) state_dict entries form the "side table" of Q elements.
+ *   - reductions run strictly in arrival order per element (k = 0, 1, ..., K-1), in fp32 with IEEE
+ *     round-to-nearest per operation and no fused multiply-add, so they are bit-identical to the
+ *     reference's numpy/torch CPU arithmetic; chunked calls (FA_ACCUMULATE) continue the same chain.
+ */
+#ifndef FEDAGG_H
+#define FEDAGG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* fa_stream_t; /* hipStream_t */
+
+enum {
+  FA_OK = 0,
+  FA_E_ARG = -1,      /* bad size / null / alignment */
+  FA_E_HIP = -2,      /* a HIP runtime call failed */
+  FA_E_RANGE = -3,    /* size beyond what the kernel supports */
+};
+
+/* flags for fa_reduce / fa_reduce_yogi */
+enum {
+  FA_ACCUMULATE = 1, /* chain starts from acc_in[p] (a previous chunk) instead of client 0 */
+  FA_FINALIZE = 2,   /* write chain / denom (true fp32 division) instead of the raw chain */
+  FA_YOGI_INIT = 4,  /* fa_reduce_yogi / fa_yogi_step: first call, m := 0 and v := tau (yogi.py:17-19) */
+};
+
+int fa_abi_version(void);
+const char* fa_last_error_string(void);
+
+/*
+ * Weighted in-order K-way column reduction over one chunk of K client updates.
+ *   chain_p = FA_ACCUMULATE ? acc_in[p] : w_0*x[0][p]      (w_k = a[k], or 1 when a == NULL)
+ *   chain_p = chain_p + w_k*x[k][p]                          k = (FA_ACCUMULATE ? 0 : 1) .. K-1
+ *   out[p]  = FA_FINALIZE ? chain_p / denom : chain_p
+ * Replaces: Aggregator.update_weight_aggregation, aggregator.py:489-511 (a == NULL, denom = K) and
+ *           AsyncAggregator.update_weight_aggregation, async_aggregator.py:115-137 (a = staleness
+ *           weights 1/sqrt(1+s) rounded to fp32, denom = fp32(sum of the weights)).
+ * `a` is a device array of K fp32 weights or NULL.  out may alias acc_in.
+ */
+int fa_reduce(const float* x, int64_t ld, int32_t K, int64_t P, const float* a, const float* acc_in,
+              float* out, float denom, int32_t flags, fa_stream_t stream);
+
+/*
+ * fa_reduce with FA_FINALIZE, fused with the FedYoGi server step in the same pass over HBM:
+ *   cur = chain/denom; g = cur - last; m = beta*m + omb*g; v = v - (omb2*g*g)*sign(v - g*g);
+ *   out = last + (reciprocal(sqrt(v) + tau) * eta) * m
+ * Replaces: TorchModelAdapter.set_weights (torch_model_adapter.py:23-39) ->
+ *           TorchServerOptimizer.update_round_gradient fed-yogi branch (optimizers.py:43-63) ->
+ *           YoGi.update (yogi.py:15-36).  omb = fp32(1-beta), omb2 = fp32(1-beta2) as the host computes
+ *           them in double.  m, v are updated in place; FA_YOGI_INIT ignores their contents.
+ *           mean_out (optional, may be NULL) receives cur, the FedAvg mean the reference keeps in
+ *           Aggregator.model_weights.
+ */
+int fa_reduce_yogi(const float* x, int64_t ld, int32_t K, int64_t P, const float* a, const float* acc_in,
+                   float denom, const float* last, float* m, float* v, float* out, float* mean_out, float eta,
+                   float tau, float beta, float omb, float omb2, int32_t flags, fa_stream_t stream);
+
+/* The FedYoGi step alone on an already-reduced model (cur = the new mean), same arithmetic as above.
+ * Replaces: optimizers.py:43-63 + yogi.py:15-36 when set_weights() is handed a list of weights. */
+int fa_yogi_step(const float* cur, const float* last, float* m, float* v, float* out, int64_t P, float eta,
+                 float tau, float beta, float omb, float omb2, int32_t flags, fa_stream_t stream);
+
+/*
+ * q-FedAvg phase 1 over one chunk of K (<= fa_qfed_max_chunk()) retained client updates:
+ *   g_k = (last - x[k]) / lr                      (fp32 true division)
+ *   delta = FA_ACCUMULATE ? delta + alpha_k*g_0 : alpha_0*g_0; delta = delta + alpha_k*g_k ...
+ *   sqnorm[k] += sum_p fp32(g_k[p]^2)              (accumulated in fp64, deterministic order)
+ * Replaces: the per-client loop of optimizers.py:73-98 (client results retained at aggregator.py:466-467).
+ * alpha: device fp32[K] = fp32(float_power(loss_k + 1e-10, q)).  sqnorm: device fp64[K].
+ * workspace: device memory of fa_qfed_workspace_bytes(K) bytes.
+ */
+int fa_qfed_max_chunk(void);
+int64_t fa_qfed_workspace_bytes(int32_t K);
+int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t P, const float* last, const float* alpha,
+                       float lr, float* delta, double* sqnorm, void* workspace, int32_t flags,
+                       fa_stream_t stream);
+
+/*
+ * q-FedAvg Lipschitz estimate, the fp32 recurrence of optimizers.py:96-98 in arrival order:
+ *   hs = 0; hs = hs + (c1[k]*fp32(sqnorm[k]) + c2[k])      k = 0..K-1
+ *   hs_out[0] = hs; hs_out[1] = hs + fp32(1e-10)          (the divisor of optimizers.py:102)
+ * c1[k] = fp32(q*float_power(loss_k+1e-10, q-1)), c2[k] = fp32((1/lr)*float_power(loss_k+1e-10, q)).
+ */
+int fa_qfed_hs(const double* sqnorm, const float* c1, const float* c2, int32_t K, float* hs_out,
+               fa_stream_t stream);
+
+/* q-FedAvg phase 2: out = last - delta / hs_dev[1]  (optimizers.py:101-104). */
+int fa_qfed_finalize(const float* last, const float* delta, const float* hs_dev, float* out, int64_t P,
+                     fa_stream_t stream);
+
+/*
+ * Side table (non-fp32 state_dict entries, BatchNorm num_batches_tracked etc.).
+ * xi: device int64 [K][Q] client-major.  State: acc_i (int64 [Q]) and acc_d (fp64 [Q]).
+ *   mode 0 FedAvg : acc_i = acc_i + xi[k]  (int64, aggregator.py:500-503)
+ *   mode 1 FedBuff: acc_d = acc_d + w[k]*double(xi[k]), first = double(xi[0])*w[0] (async_aggregator.py:129-133)
+ * w: device fp64[K] or NULL.  FA_ACCUMULATE continues a previous chunk.
+ */
+int fa_side_accumulate(const int64_t* xi, int32_t ldq, int32_t K, int32_t Q, int32_t mode, const double* w,
+                       int64_t* acc_i, double* acc_d, int32_t flags, fa_stream_t stream);
+/* cur[q] = (mode 0 ? double(acc_i) : acc_d) / denom  (np.divide -> float64, aggregator.py:505-507) and
+ * model[q] = int64(fp32(cur[q]))  (np.asarray(float32) + load_state_dict truncation, torch_model_adapter.py:31-35). */
+int fa_side_close(const int64_t* acc_i, const double* acc_d, int32_t Q, int32_t mode, double denom, double* cur,
+                  int64_t* model, fa_stream_t stream);
+/* FedYoGi on the side table, in fp64 (int64 - float64 promotes, optimizers.py:52-61, yogi.py:15-36):
+ * g = cur - double(last) (last NULL -> 0); step = (reciprocal(sqrt(v)+tau)*eta)*m;
+ * step[q] (optional) = step; model[q] (optional) = int64(fp32(double(last) + step)).  m, v: fp64 [Q]. */
+int fa_side_yogi(const double* cur, const int64_t* last, double* m, double* v, double* step, int64_t* model,
+                 int32_t Q, double eta, double tau, double beta, double omb, double omb2, int32_t flags,
+                 fa_stream_t stream);
+/* q-FedAvg on the side table: per element the delta chain over the chunk (fp32), per client the
+ * fp64-accumulated sum of fp32 g^2 added to sqnorm[k]. delta_s: fp32 [Q]. */
+int fa_side_qfed_accumulate(const int64_t* xi, int32_t ldq, int32_t K, int32_t Q, const int64_t* last,
+                            const float* alpha, float lr, float* delta_s, double* sqnorm, int32_t flags,
+                            fa_stream_t stream);
+/* model[q] = int64( fp32(last[q]) - delta_s[q] / hs_dev[1] ) */
+int fa_side_qfed_finalize(const int64_t* last, const float* delta_s, const float* hs_dev, int64_t* model,
+                          int32_t Q, fa_stream_t stream);
+
+/*
+ * Deterministic synthetic client updates for benchmarks and full-size parity tests:
+ *   x[k][p] = base(p) + noise(k, p), base ~ scale_base * tri(seed, p), noise ~ scale_noise * tri(seed+1+k0+k, p)
+ * where tri() is a triangular variate built from a 32-bit integer hash (bit-reproducible on the host,
+ * see fedscale_amd/synth.py).  Columns [P, ld) are zero-filled.
+ */
+int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uint32_t seed, int32_t k0, float scale_base,
+                      float scale_noise, fa_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEDAGG_H */

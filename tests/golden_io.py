@@ -89,3 +89,38 @@ def assert_state_equal(got, want, ctx=""):
             bad = np.argwhere(g != w)
             raise AssertionError(f"{ctx} tensor {i}: {len(bad)} mismatches, first at {bad[:3].tolist()}: "
                                  f"got {g[tuple(bad[0])] if g.ndim else g} want {w[tuple(bad[0])] if w.ndim else w}")
+
+
+class StateDictModule(torch.nn.Module):
+    """Minimal nn.Module exposing a fixed, ordered state_dict (names may contain dots)."""
+
+    def __init__(self, names, tensors):
+        super().__init__()
+        from collections import OrderedDict
+
+        self._sd = OrderedDict((n, t.detach().clone()) for n, t in zip(names, tensors))
+
+    def state_dict(self, *a, **k):
+        return self._sd
+
+    def load_state_dict(self, new, strict=True):
+        for n, dst in self._sd.items():
+            dst.copy_(new[n])
+
+
+def assert_state_close(got, want, rtol, ctx="", int_slack=0):
+    """Per-tensor: |got - want| <= rtol * max(|want|, rms(want)) elementwise; ints within int_slack."""
+    for i, (g, w) in enumerate(zip(got, want)):
+        g = g.detach().cpu().numpy() if torch.is_tensor(g) else np.asarray(g)
+        w = np.asarray(w)
+        assert g.dtype == w.dtype and g.shape == w.shape, f"{ctx} tensor {i}: {g.dtype}{g.shape} vs {w.dtype}{w.shape}"
+        if w.size == 0:
+            continue
+        if np.issubdtype(w.dtype, np.integer):
+            assert np.max(np.abs(g.astype(np.int64) - w.astype(np.int64))) <= int_slack, f"{ctx} tensor {i}"
+            continue
+        wd = w.astype(np.float64)
+        scale = np.maximum(np.abs(wd), np.sqrt(np.mean(wd * wd)))
+        err = np.abs(g.astype(np.float64) - wd)
+        bad = err > rtol * scale
+        assert not bad.any(), f"{ctx} tensor {i}: {bad.sum()} elements beyond rtol={rtol}, max rel {np.max(err / np.maximum(scale, 1e-30)):.3g}"

@@ -1,0 +1,115 @@
+"""CPU-only checks: the C ABI library loads and exports every symbol of include/fedagg.h, the host-side
+layout / packing / sharding logic, the host twin of the synthetic generator, and that the product
+package never reaches into oracle/."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _header_functions():
+    src = open(os.path.join(ROOT, "include", "fedagg.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(fa_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from fedscale_amd import _native
+
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    names = _header_functions()
+    assert len(names) >= 16
+    for n in names:
+        assert hasattr(lib, n), f"{n} declared in include/fedagg.h but not exported"
+    assert sorted(_native.SIGNATURES) == names, "ctypes binding out of sync with include/fedagg.h"
+    _native.load()  # types every entry point, checks the ABI version (no GPU call)
+    assert _native.load().fa_abi_version() == _native.ABI_VERSION
+
+
+def test_error_path_without_gpu():
+    from fedscale_amd._native import FedAggError, call
+
+    with pytest.raises(FedAggError, match="ld"):
+        call("fa_reduce", None, 6, 1, 8, None, None, None, 1.0, 2, None)  # validation precedes any HIP call
+
+
+def test_kernels_reject_host_tensors():
+    from fedscale_amd import kernels as kx
+
+    x = torch.zeros(2, 64)
+    with pytest.raises(ValueError, match="device tensor"):
+        kx.reduce(x, 2, 64, torch.zeros(64))
+
+
+def test_layout_and_sharding():
+    from fedscale_amd.bucket import BucketLayout
+
+    names = ["a", "n", "b", "c"]
+    shapes = [(3, 5), (), (1000,), (7,)]
+    dtypes = [torch.float32, torch.int64, torch.float32, torch.float32]
+    full = BucketLayout(names, shapes, dtypes)
+    assert full.P_full == 15 + 1000 + 7 and full.Q == 1 and full.P == full.P_full
+    assert full.ld % 64 == 0 and full.ld >= full.P
+    for world in (2, 3, 4, 8):
+        shards = [BucketLayout(names, shapes, dtypes, r, world) for r in range(world)]
+        assert all(s.ld == shards[0].ld and s.ld % 64 == 0 for s in shards)
+        assert sum(s.P for s in shards) == full.P_full
+        assert shards[0].p0 == 0 and all(shards[i].p1 == shards[i + 1].p0 or shards[i + 1].P == 0
+                                         for i in range(world - 1))
+    with pytest.raises(NotImplementedError):
+        BucketLayout(["h"], [(2,)], [torch.float16])
+
+
+def test_pack_host_roundtrip_and_shards():
+    from fedscale_amd.bucket import BucketLayout
+
+    rng = np.random.default_rng(0)
+    names = ["w", "cnt", "b", "s0", "e"]
+    vals = [rng.normal(size=(33, 7)).astype(np.float32), np.array(12, dtype=np.int64),
+            rng.normal(size=(129,)).astype(np.float32), np.float32(0.25), np.zeros(0, np.float32)]
+    shapes = [np.shape(v) for v in vals]
+    dtypes = [torch.float32, torch.int64, torch.float32, torch.float32, torch.float32]
+    world = 3
+    parts = []
+    for r in range(world):
+        lay = BucketLayout(names, shapes, dtypes, r, world)
+        f = np.zeros(lay.ld, np.float32)
+        i = np.zeros(lay.ldq, np.int64)
+        lay.pack_host(lay.values_of(dict(zip(names, vals))), f, i)
+        parts.append(f)
+        assert i[0] == 12
+    flat = torch.from_numpy(np.concatenate(parts))
+    out = BucketLayout(names, shapes, dtypes).unpack(flat, torch.tensor([12]))
+    for o, v in zip(out, vals):
+        np.testing.assert_array_equal(o.numpy(), np.asarray(v))
+    lay = BucketLayout(names, shapes, dtypes)
+    with pytest.raises(TypeError):
+        lay.pack_host([v.astype(np.float64) if i == 0 else v for i, v in enumerate(vals)],
+                      np.zeros(lay.ld, np.float32), np.zeros(1, np.int64))
+    with pytest.raises(ValueError):
+        lay.pack_host(vals[:-1], np.zeros(lay.ld, np.float32), np.zeros(1, np.int64))
+
+
+def test_synth_host_twin_properties():
+    from fedscale_amd import synth
+
+    v = synth.host_columns(7, [0, 1, 2], np.arange(10000))
+    assert v.dtype == np.float32 and v.shape == (3, 10000)
+    assert np.all(np.abs(v) < 0.0601)
+    assert abs(float(v.mean())) < 2e-3
+    np.testing.assert_array_equal(v, synth.host_columns(7, [0, 1, 2], np.arange(10000)))
+    assert not np.array_equal(v[0], v[1])
+
+
+def test_product_never_imports_oracle():
+    pkg = os.path.join(ROOT, "fedscale_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), f"{f} imports oracle"

@@ -1,0 +1,246 @@
+"""GPU parity: the HIP path (through the C ABI) against the golden fixtures of the real reference and
+the CPU oracle.  Bit-exact for FedAvg / FedBuff / FedYoGi (the kernels reproduce the reference's fp32
+op order); q-FedAvg within rtol 1e-5 (BASELINE north_star tolerance) because torch's CPU sum order
+for ||g||^2 is implementation-defined — its delta chain is checked bit-exact separately."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.cpu_reference import OracleYoGi, fedavg_flat, fedbuff_flat
+from tests.golden_io import (Scenario, StateDictModule, assert_state_close, assert_state_equal,
+                             scenario_names)
+
+pytestmark = pytest.mark.gpu
+
+QFED_RTOL = 1e-5
+
+
+def _device_run(sc, capacity=None):
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator, DeviceAsyncAggregator
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    args = sc.args()
+    model = StateDictModule(sc.names, sc.init_state())
+    opt = TorchServerOptimizer(args.gradient_policy, args, "cuda:0") if sc.meta.get("optimizer") is not None else None
+    adapter = TorchModelAdapter(model, optimizer=opt, device="cuda:0", staging_capacity=capacity)
+    policy = sc.meta["policy"]
+    if policy == "fedbuff":
+        agg = DeviceAsyncAggregator(adapter, args)
+        agg.round = sc.meta["round"]
+        for k, s in enumerate(sc.meta["staleness"]):
+            agg.client_task_model_version[101 + k] = agg.round - s
+    else:
+        agg = DeviceAggregator(adapter, args)
+    for r, ks in sc.rounds():
+        if policy == "q-fedavg":
+            args.learning_rate = sc.meta["lrs"][r]
+        agg.start_round(len(ks))
+        for res in sc.results(ks, r):
+            agg.on_result(res)
+        yield r, adapter, opt, agg
+
+
+@pytest.mark.parametrize("capacity", [None, 2])
+@pytest.mark.parametrize("name", scenario_names())
+def test_device_path_matches_reference_fixture(gpu_device, name, capacity):
+    sc = Scenario(name)
+    for r, adapter, opt, agg in _device_run(sc, capacity):
+        got = adapter.get_weights()
+        if sc.meta["policy"] == "q-fedavg":
+            assert_state_close(got, sc.expected(r), QFED_RTOL, f"{name} r{r}", int_slack=1)
+        else:
+            assert_state_equal(got, sc.expected(r), f"{name} r{r} cap={capacity}")
+        if sc.meta["policy"] == "fed-yogi":
+            m, v = sc.yogi_state(r)
+            assert_state_equal(opt.gradient_controller.m_t, m, f"{name} m r{r}")
+            assert_state_equal(opt.gradient_controller.v_t, v, f"{name} v r{r}")
+
+
+def test_model_weights_is_the_fedavg_mean(gpu_device):
+    """Aggregator.model_weights after the last result = the mean (aggregator.py:505-507), lazily fetched."""
+    sc = Scenario("fedavg_mixed_k7")
+    from oracle.cpu_reference import fedavg_close, fedavg_step
+
+    acc = None
+    for k in range(7):
+        acc = fedavg_step(acc, sc.client(k), k == 0)
+    want = fedavg_close(acc, 7)
+    for _, adapter, _, agg in _device_run(sc):
+        got = list(agg.model_weights)
+        for g, w in zip(got, want):
+            np.testing.assert_array_equal(np.asarray(g), np.asarray(w))
+            assert np.asarray(g).dtype == np.asarray(w).dtype
+
+
+def test_get_model_syncs_module(gpu_device):
+    sc = Scenario("fedavg_femnist_cnn_k10")
+    for r, adapter, _, _ in _device_run(sc):
+        m = adapter.get_model()
+        assert_state_equal(list(m.state_dict().values()), sc.expected(r), "get_model")
+
+
+def test_reference_typed_optimizer_api(gpu_device):
+    """TorchServerOptimizer.update_round_gradient with the reference's list/nn.Module types."""
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+    from oracle.cpu_reference import OracleModel, OracleServerOptimizer
+
+    sc = Scenario("fedyogi_mixed_3rounds")
+    args = sc.args()
+    ours = TorchServerOptimizer("fed-yogi", args, None)
+    theirs = OracleServerOptimizer("fed-yogi", args, None)
+    m_ours = StateDictModule(sc.names, sc.init_state())
+    m_theirs = OracleModel(sc.names, sc.init_state())
+    rng = np.random.default_rng(5)
+    for r in range(3):
+        last = [t.clone() for t in m_theirs.state_dict().values()]
+        cur = []
+        for t in last:
+            if t.dtype == torch.int64:
+                cur.append(t.to(torch.float64) + float(rng.integers(0, 4)) / 3)
+            else:
+                cur.append(t + torch.from_numpy(rng.normal(0, 0.01, size=tuple(t.shape)).astype(np.float32)))
+        ours.update_round_gradient([t.clone() for t in last], [c.clone() for c in cur], m_ours)
+        theirs.update_round_gradient(last, cur, m_theirs)
+        assert_state_equal(list(m_ours.state_dict().values()), list(m_theirs.state_dict().values()), f"round {r}")
+
+
+def test_yogi_update_api_matches_oracle(gpu_device):
+    """YoGi.update(list) -> list of steps, 3 calls with state carry-over, fp32 and fp64 gradients."""
+    from fedscale_amd.utils.optimizer.yogi import YoGi
+
+    ours, theirs = YoGi(3e-3, 1e-8, 0.9, 0.99), OracleYoGi(3e-3, 1e-8, 0.9, 0.99)
+    rng = np.random.default_rng(0)
+    shapes = [(17, 5), (3,), (), (64,), (1,)]
+    for it in range(3):
+        grads = [torch.from_numpy(rng.normal(0, 0.02, size=s).astype(np.float32)) for s in shapes]
+        grads.append(torch.tensor(float(it) + 0.5, dtype=torch.float64))
+        got = ours.update([g.cuda() for g in grads])
+        want = theirs.update(grads)
+        assert_state_equal([g.cpu() for g in got], [w.numpy() for w in want], f"step {it}")
+        assert_state_equal([t.cpu() for t in ours.m_t], [t.numpy() for t in theirs.m_t], f"m {it}")
+        assert_state_equal([t.cpu() for t in ours.v_t], [t.numpy() for t in theirs.v_t], f"v {it}")
+
+
+# ---------------------------------------------------------------------------------------------
+# kernel level, random inputs, edge shapes
+# ---------------------------------------------------------------------------------------------
+@pytest.mark.parametrize("K", [1, 2, 3, 7, 8, 9, 17, 64])
+@pytest.mark.parametrize("P", [1, 3, 4, 5, 63, 64, 65, 1000, 4099, 70001])
+def test_reduce_kernel_bit_exact(gpu_device, K, P):
+    from fedscale_amd import kernels as kx
+    from fedscale_amd.bucket import round_up
+
+    rng = np.random.default_rng(K * 100003 + P)
+    ld = round_up(P, 64)
+    xh = np.zeros((K, ld), dtype=np.float32)
+    xh[:, :P] = rng.normal(0.1, 1.0, size=(K, P)).astype(np.float32)
+    x = torch.from_numpy(xh).cuda()
+    out = torch.full((ld,), 7.0, device="cuda")
+    kx.reduce(x, K, P, out, denom=float(np.float32(K)), finalize=True)
+    np.testing.assert_array_equal(out[:P].cpu().numpy(), fedavg_flat(xh[:, :P]))
+    # weighted (FedBuff) and chunked continuation
+    s = [1 / (1 + (k % 6)) ** 0.5 for k in range(K)]
+    a = torch.tensor(np.asarray(s, dtype=np.float32), device="cuda")
+    acc = torch.zeros(ld, device="cuda")
+    h = K // 2
+    if h:
+        kx.reduce(x[:h], h, P, acc, a=a[:h])
+        kx.reduce(x[h:], K - h, P, acc, a=a[h:], acc_in=acc, denom=float(np.float32(sum(s))), finalize=True)
+    else:
+        kx.reduce(x, K, P, acc, a=a, denom=float(np.float32(sum(s))), finalize=True)
+    np.testing.assert_array_equal(acc[:P].cpu().numpy(), fedbuff_flat(xh[:, :P], s))
+    # untouched tail: out[P:] beyond the float4 columns is not written
+    if ld > (P + 3) // 4 * 4:
+        assert float(out[ld - 1]) == 7.0
+
+
+def test_reduce_kernel_special_values(gpu_device):
+    from fedscale_amd import kernels as kx
+
+    K, P = 5, 256
+    xh = np.random.default_rng(1).normal(size=(K, P)).astype(np.float32)
+    xh[0, 0] = np.inf
+    xh[1, 1] = np.nan
+    xh[:, 2] = [3e38, 3e38, -3e38, 0, 0]       # overflow then back: inf - inf
+    xh[:, 3] = [1e-45, 1e-45, 0, 0, 0]         # denormals
+    xh[:, 4] = [-0.0] * K
+    x = torch.from_numpy(xh).cuda()
+    out = torch.empty(P, device="cuda")
+    kx.reduce(x, K, P, out, denom=5.0, finalize=True)
+    with np.errstate(all="ignore"):
+        want = fedavg_flat(xh)
+    got = out.cpu().numpy()
+    np.testing.assert_array_equal(got, want)
+    assert np.signbit(got[4]) == np.signbit(want[4])
+
+
+def test_qfed_kernels_delta_bit_exact_and_hs(gpu_device):
+    from fedscale_amd import kernels as kx
+
+    rng = np.random.default_rng(3)
+    K, P, ld = 37, 100003, 100032
+    L = rng.normal(0, 0.05, size=ld).astype(np.float32)
+    L[P:] = 0
+    xh = (L[None, :] + rng.normal(0, 0.01, size=(K, ld))).astype(np.float32)
+    xh[:, P:] = 0
+    losses = rng.uniform(0.5, 2.0, size=K)
+    lr, q = 0.05, 1.0
+    alpha = np.array([np.float32(np.float_power(l + 1e-10, q)) for l in losses], dtype=np.float32)
+    x = torch.from_numpy(xh).cuda()
+    Ld = torch.from_numpy(L).cuda()
+    delta = torch.zeros(ld, device="cuda")
+    sq = torch.zeros(K, dtype=torch.float64, device="cuda")
+    ws = kx.qfed_workspace(K, "cuda")
+    h = 20
+    kx.qfed_accumulate(x[:h], h, P, last=Ld, alpha=torch.from_numpy(alpha[:h]).cuda(), lr=lr, delta=delta,
+                       sqnorm=sq[:h], workspace=ws, accumulate=False)
+    kx.qfed_accumulate(x[h:], K - h, P, last=Ld, alpha=torch.from_numpy(alpha[h:]).cuda(), lr=lr, delta=delta,
+                       sqnorm=sq[h:], workspace=ws, accumulate=True)
+    # host emulation of optimizers.py:82-93 in fp32
+    d = None
+    sq_ref = np.zeros(K)
+    for k in range(K):
+        g = (L[:P] - xh[k, :P]) / np.float32(lr)
+        t = alpha[k] * g
+        d = t if d is None else d + t
+        sq_ref[k] = np.sum((g * g).astype(np.float64))
+    np.testing.assert_array_equal(delta[:P].cpu().numpy(), d)
+    np.testing.assert_allclose(sq.cpu().numpy(), sq_ref, rtol=1e-12)
+    # hs recurrence (fp32, arrival order) is bit-exact given the same sqnorm
+    c1 = np.array([np.float32(q * np.float_power(l + 1e-10, q - 1)) for l in losses], dtype=np.float32)
+    c2 = np.array([np.float32((1.0 / lr) * np.float_power(l + 1e-10, q)) for l in losses], dtype=np.float32)
+    hs = torch.zeros(2, device="cuda")
+    kx.qfed_hs(sq, torch.from_numpy(c1).cuda(), torch.from_numpy(c2).cuda(), K, hs)
+    s32 = sq.cpu().numpy().astype(np.float32)
+    hh = np.float32(0)
+    for k in range(K):
+        hh = np.float32(hh + np.float32(c1[k] * s32[k] + c2[k]))
+    assert hs[0].item() == float(hh)
+    assert hs[1].item() == float(np.float32(hh + np.float32(1e-10)))
+
+
+def test_synthetic_generator_matches_host_twin(gpu_device):
+    from fedscale_amd import synth
+
+    K, P, ld = 5, 10007, 10048
+    x = torch.empty(K, ld, device="cuda")
+    synth.fill(x, K, P, seed=1234, k0=17)
+    cols = np.array([0, 1, 2, 3, 4095, 4096, 10006])
+    want = synth.host_columns(1234, range(17, 17 + K), cols)
+    np.testing.assert_array_equal(x[:, cols].cpu().numpy(), want)
+    assert float(x[:, P:].abs().sum()) == 0.0
+
+
+def test_errors_are_loud(gpu_device):
+    from fedscale_amd import kernels as kx
+    from fedscale_amd._native import FedAggError, call
+
+    x = torch.zeros(2, 64, device="cuda")
+    out = torch.zeros(64, device="cuda")
+    with pytest.raises(TypeError):
+        kx.reduce(x.double(), 2, 64, out)
+    with pytest.raises(ValueError):
+        kx.reduce(x.cpu(), 2, 64, out)
+    with pytest.raises(FedAggError):  # the C ABI itself rejects a misaligned pointer
+        call("fa_reduce", x.data_ptr() + 4, 64, 2, 60, None, None, out.data_ptr(), 1.0, 2, None)
