@@ -1,7 +1,15 @@
 """GPU parity: the HIP path (through the C ABI) against the golden fixtures of the real reference and
-the CPU oracle.  Bit-exact for FedAvg / FedBuff / FedYoGi (the kernels reproduce the reference's fp32
-op order); q-FedAvg within rtol 1e-5 (BASELINE north_star tolerance) because torch's CPU sum order
-for ||g||^2 is implementation-defined — its delta chain is checked bit-exact separately."""
+the CPU oracle.
+
+* FedAvg / FedBuff (and the int64 side table): bit-exact — the kernels reproduce the reference's fp32
+  op order (sequential arrival-order sum, true division, no FMA).
+* FedYoGi: m and v bit-exact whenever they depend on the inputs only; the new model within
+  YOGI_RTOL = 1e-6.  Reason: the reference's ``torch.sqrt`` on the CPU is not IEEE-correctly rounded
+  (this torch build dispatches it to MKL VML; 0.7 % of fp32 inputs come out 1 ulp low, see
+  tests/test_numerics_notes.py), while the GPU kernel uses the correctly rounded sqrt.
+* q-FedAvg: within QFED_RTOL = 1e-5 (the north-star tolerance) because torch's CPU sum order for
+  ||g||^2 is implementation-defined; the delta chain and the hs recurrence are checked bit-exact
+  separately (test_qfed_kernels_delta_bit_exact_and_hs)."""
 import numpy as np
 import pytest
 import torch
@@ -13,6 +21,7 @@ from tests.golden_io import (Scenario, StateDictModule, assert_state_close, asse
 pytestmark = pytest.mark.gpu
 
 QFED_RTOL = 1e-5
+YOGI_RTOL = 1e-6
 
 
 def _device_run(sc, capacity=None):
@@ -49,12 +58,17 @@ def test_device_path_matches_reference_fixture(gpu_device, name, capacity):
         got = adapter.get_weights()
         if sc.meta["policy"] == "q-fedavg":
             assert_state_close(got, sc.expected(r), QFED_RTOL, f"{name} r{r}", int_slack=1)
+        elif sc.meta["policy"] == "fed-yogi":
+            assert_state_close(got, sc.expected(r), YOGI_RTOL, f"{name} r{r}")
+            m, v = sc.yogi_state(r)
+            if r == 0:  # before any sqrt-dependent value feeds back
+                assert_state_equal(opt.gradient_controller.m_t, m, f"{name} m r{r}")
+                assert_state_equal(opt.gradient_controller.v_t, v, f"{name} v r{r}")
+            else:
+                assert_state_close(opt.gradient_controller.m_t, m, YOGI_RTOL, f"{name} m r{r}")
+                assert_state_close(opt.gradient_controller.v_t, v, YOGI_RTOL, f"{name} v r{r}")
         else:
             assert_state_equal(got, sc.expected(r), f"{name} r{r} cap={capacity}")
-        if sc.meta["policy"] == "fed-yogi":
-            m, v = sc.yogi_state(r)
-            assert_state_equal(opt.gradient_controller.m_t, m, f"{name} m r{r}")
-            assert_state_equal(opt.gradient_controller.v_t, v, f"{name} v r{r}")
 
 
 def test_model_weights_is_the_fedavg_mean(gpu_device):
@@ -102,7 +116,10 @@ def test_reference_typed_optimizer_api(gpu_device):
                 cur.append(t + torch.from_numpy(rng.normal(0, 0.01, size=tuple(t.shape)).astype(np.float32)))
         ours.update_round_gradient([t.clone() for t in last], [c.clone() for c in cur], m_ours)
         theirs.update_round_gradient(last, cur, m_theirs)
-        assert_state_equal(list(m_ours.state_dict().values()), list(m_theirs.state_dict().values()), f"round {r}")
+        assert_state_close(list(m_ours.state_dict().values()), list(m_theirs.state_dict().values()), YOGI_RTOL,
+                           f"round {r}")
+        # keep both on the same trajectory (the reference's sqrt is not IEEE: see module docstring)
+        m_ours.load_state_dict(dict(m_theirs.state_dict()))
 
 
 def test_yogi_update_api_matches_oracle(gpu_device):
@@ -117,7 +134,7 @@ def test_yogi_update_api_matches_oracle(gpu_device):
         grads.append(torch.tensor(float(it) + 0.5, dtype=torch.float64))
         got = ours.update([g.cuda() for g in grads])
         want = theirs.update(grads)
-        assert_state_equal([g.cpu() for g in got], [w.numpy() for w in want], f"step {it}")
+        assert_state_close([g.cpu() for g in got], [w.numpy() for w in want], YOGI_RTOL, f"step {it}")
         assert_state_equal([t.cpu() for t in ours.m_t], [t.numpy() for t in theirs.m_t], f"m {it}")
         assert_state_equal([t.cpu() for t in ours.v_t], [t.numpy() for t in theirs.v_t], f"v {it}")
 
