@@ -50,7 +50,17 @@ extern "C" const char* fa_last_error_string(void) { return g_err; }
 // ------------------------------------------------------------------------------------------------
 // small device helpers
 // ------------------------------------------------------------------------------------------------
-__device__ __forceinline__ f4 ldnt(const f4* p) { return __builtin_nontemporal_load(p); }
+#ifndef FA_RED_NT
+#define FA_RED_NT 1
+#endif
+// client rows are read exactly once: non-temporal loads keep them from evicting L2 / Infinity Cache lines
+__device__ __forceinline__ f4 ldnt(const f4* p) {
+#if FA_RED_NT
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
 
 __device__ __forceinline__ float sgnf(float x) {  // torch.sign: -1, 0, +1 (NaN passes through)
   return x > 0.f ? 1.f : (x < 0.f ? -1.f : x);
@@ -89,6 +99,7 @@ struct RedArgs {
   const float* x;
   int64_t ld4;  // row stride in float4
   int64_t P4;   // float4 columns to produce (ceil(P/4))
+  int64_t col0; // first float4 column of this launch (a launch covers [col0, min(P4, col0 + grid*span)))
   int K;
   int flags;
   const float* a;
@@ -104,11 +115,14 @@ struct RedArgs {
 
 // V: float4 per lane per client (a wave covers V KiB contiguous of one client row)
 // U: clients loaded ahead of the adds
+#ifndef FA_RED_WAVES
+#define FA_RED_WAVES 4
+#endif
 template <int V, int U, int EPI, bool W>
-__global__ __launch_bounds__(256) void k_reduce(RedArgs r) {
+__global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int64_t c0 = ((int64_t)blockIdx.x * 4 + wave) * (64 * V) + lane;
+  const int64_t c0 = r.col0 + ((int64_t)blockIdx.x * FA_RED_WAVES + wave) * (64 * V) + lane;
   const f4* __restrict__ xp = reinterpret_cast<const f4*>(r.x);
 
   bool ok[V];
@@ -191,25 +205,87 @@ __global__ __launch_bounds__(256) void k_reduce(RedArgs r) {
   }
 }
 
-// tuned configuration (see DESIGN.md §kernels / profiles/): V float4 per lane, U clients in flight
-#ifndef FA_RED_V
-#define FA_RED_V 2
+// Launch plan.  Each wave owns a column tile of V KiB (V float4 per lane) and walks all K clients, so a
+// tile is K*V KiB of reads.  Wide tiles keep few DRAM pages open per client row (measured: V=32 reads at
+// the stream-read ceiling, V=2 ~6 % below, profiles/r01_tune_sweep.log); but with few, long tiles the
+// last wave of workgroups leaves CUs idle.  So the columns are cut into up to three launches: the
+// widest variant takes as many FULL waves of workgroups as fit (occupancy x CUs, queried at run time),
+// the next narrower variant the same on what is left, the narrowest the remainder.  Every column is
+// still reduced by exactly one thread in arrival order, so the split never changes a bit.
+#ifdef FA_RED_V  // tuning build: a single fixed variant
+#define FA_LEVELS 1
+#define FA_L0_V FA_RED_V
+#define FA_L0_U FA_RED_U
+#else
+#define FA_LEVELS 4
+#define FA_L0_V 32
+#define FA_L0_U 1
+#define FA_L1_V 16
+#define FA_L1_U 4
+#define FA_L2_V 8
+#define FA_L2_U 4
+#define FA_L3_V 2
+#define FA_L3_U 8
 #endif
-#ifndef FA_RED_U
-#define FA_RED_U 8
+
+template <int V, int U, int EPI, bool W>
+static int resident_blocks() {
+  static int cache[64];  // per device ordinal: occupancy x CU count (idempotent, benign race)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cache[dev] > 0) return cache[dev];
+  int per_cu = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_reduce<V, U, EPI, W>),
+                                                   64 * FA_RED_WAVES, 0) != hipSuccess)
+    return 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  cache[dev] = per_cu * cus;
+  return cache[dev];
+}
+
+// launch variant (V, U) over float4 columns [col, col_end); `full_waves_only` keeps only whole waves of
+// workgroups (a last partial wave is kept when it would still occupy >= 90 % of the resident slots: a
+// narrower variant is ~6 % slower per byte, so handing such a wave down costs more than its idle 10 %)
+// and returns the first column it did not cover.
+template <int V, int U, int EPI, bool W>
+static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_waves_only, hipStream_t st) {
+  const int64_t span = 64LL * FA_RED_WAVES * V;
+  int64_t nblk = (col_end - col + span - 1) / span;
+  if (full_waves_only) {
+    const int64_t R = resident_blocks<V, U, EPI, W>();
+    if (R <= 0) return col;
+    const int64_t total = nblk;  // including a partial last tile
+    nblk = ((col_end - col) / span) / R * R;
+    if (total - nblk >= (R * 9) / 10) nblk = total;  // rest < R + 1 blocks: finish it here
+  }
+  if (nblk <= 0) return col;
+  r.col0 = col;
+  hipLaunchKernelGGL((k_reduce<V, U, EPI, W>), dim3((unsigned)nblk), dim3(64 * FA_RED_WAVES), 0, st, r);
+  const int64_t end = col + nblk * span;
+  return (full_waves_only && end < col_end) ? end : col_end;
+}
+
+template <int EPI, bool W>
+static void launch_plan(const RedArgs& r, hipStream_t st) {
+  int64_t col = 0;
+#if FA_LEVELS == 1
+  launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, false, st);
+#else
+  col = launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, true, st);
+  if (col < r.P4) col = launch_level<FA_L1_V, FA_L1_U, EPI, W>(r, col, r.P4, true, st);
+  if (col < r.P4) col = launch_level<FA_L2_V, FA_L2_U, EPI, W>(r, col, r.P4, true, st);
+  if (col < r.P4) launch_level<FA_L3_V, FA_L3_U, EPI, W>(r, col, r.P4, false, st);
 #endif
+}
 
 template <int EPI>
 static int launch_reduce(const RedArgs& r, hipStream_t st, const char* what) {
-  constexpr int V = FA_RED_V, U = FA_RED_U;
-  const int64_t per_block = 256LL * V;
-  const int64_t nblk = (r.P4 + per_block - 1) / per_block;
-  if (nblk <= 0) return FA_OK;
-  if (nblk > 0x7fffffffLL) return fail(FA_E_RANGE, "%s: P too large (%lld blocks)", what, (long long)nblk);
+  if (r.P4 <= 0) return FA_OK;
+  if (r.P4 / (64 * FA_RED_WAVES) > 0x7fffffffLL) return fail(FA_E_RANGE, "%s: P too large", what);
   if (r.a)
-    hipLaunchKernelGGL((k_reduce<V, U, EPI, true>), dim3((unsigned)nblk), dim3(256), 0, st, r);
+    launch_plan<EPI, true>(r, st);
   else
-    hipLaunchKernelGGL((k_reduce<V, U, EPI, false>), dim3((unsigned)nblk), dim3(256), 0, st, r);
+    launch_plan<EPI, false>(r, st);
   return check_launch(what);
 }
 

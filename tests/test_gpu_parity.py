@@ -143,7 +143,7 @@ def test_yogi_update_api_matches_oracle(gpu_device):
 # kernel level, random inputs, edge shapes
 # ---------------------------------------------------------------------------------------------
 @pytest.mark.parametrize("K", [1, 2, 3, 7, 8, 9, 17, 64])
-@pytest.mark.parametrize("P", [1, 3, 4, 5, 63, 64, 65, 1000, 4099, 70001])
+@pytest.mark.parametrize("P", [1, 3, 4, 5, 63, 64, 65, 1000, 4099, 70001, 8_400_017])
 def test_reduce_kernel_bit_exact(gpu_device, K, P):
     from fedscale_amd import kernels as kx
     from fedscale_amd.bucket import round_up

@@ -27,3 +27,22 @@ if [[ $STAGE == all || $STAGE == prof ]]; then
   tail -1 $OUT/prof.log
   find $OUT/prof -name "*kernel_stats.csv" | head -3
 fi
+if [[ $STAGE == pmc ]]; then
+  export TMPDIR=/tmp
+  ARGS="--steps 3 --warmup 1 --cpu-seconds 0"
+  timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $ROOT/bench.py $ARGS > $OUT/pmc_fetch.log 2>&1 || { tail -20 $OUT/pmc_fetch.log; exit 1; }
+  timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $ROOT/bench.py $ARGS > $OUT/pmc_write.log 2>&1 || { tail -20 $OUT/pmc_write.log; exit 1; }
+  python tools/pmc_parse.py $OUT/pmc_fetch $OUT/pmc_write fedavg_k1000_p25000000 $((4*1000*25000000 + 4*25000000)) && cp profiles/pmc_traffic.json $OUT/
+fi
+if [[ $STAGE == tune ]]; then
+  timeout -k 10 300 python tools/hbm_ceiling.py 64 > $OUT/ceiling.log 2>&1 || { tail -20 $OUT/ceiling.log; exit 1; }
+  cat $OUT/ceiling.log
+  timeout -k 10 900 python tools/tune_reduce.py 1000 25000000 5 > $OUT/tune.log 2>&1 || { tail -20 $OUT/tune.log; exit 1; }
+  cat $OUT/tune.log
+  timeout -k 10 600 python tools/tune_reduce.py 100 1000000 7 > $OUT/tune_c2.log 2>&1 || { tail -20 $OUT/tune_c2.log; exit 1; }
+  cat $OUT/tune_c2.log
+fi
+if [[ $STAGE == sweep ]]; then
+  timeout -k 10 1000 python tools/tune_reduce.py sweep ${SWEEP:-1000:25000000,1000:11191242,1000:12500000,400:50000000,1000:4000000,100:1000000} 3 > $OUT/sweep.log 2>&1 || { tail -20 $OUT/sweep.log; exit 1; }
+  cat $OUT/sweep.log
+fi
