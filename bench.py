@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--reassemble", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample (0 = skip)")
     ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse ranks sharing a GPU")
     return ap.parse_args()
 
 
@@ -87,10 +89,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    local_dev = local if args.dist_backend == "nccl" else local % max(1, ndev)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    from fedscale_amd.state import ShardGroup
+
+    shards = ShardGroup(rank, world)
 
     from fedscale_amd import kernels as kx
     from fedscale_amd import synth
@@ -146,20 +156,19 @@ def main():
 
     reassembly_ms = None
     if args.reassemble and world > 1:
-        gathered = torch.empty(world * ld, dtype=torch.float32, device=dev)
-        dist.all_gather_into_tensor(gathered, out)
+        shards.all_gather(out)  # warm the communicator
         torch.cuda.synchronize(dev)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         dist.barrier()
-        e0.record(stream)
+        t0r = time.perf_counter()
         for _ in range(5):
-            dist.all_gather_into_tensor(gathered, out)
-        e1.record(stream)
+            gathered = shards.all_gather(out)
         torch.cuda.synchronize(dev)
-        reassembly_ms = e0.elapsed_time(e1) / 5
+        reassembly_ms = (time.perf_counter() - t0r) * 1e3 / 5
 
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall, kern_ms], dtype=torch.float64)
     if world > 1:
+        if args.dist_backend == "nccl":
+            t = t.to(dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall, kern_ms_max = float(t[0]), float(t[1])
 

@@ -39,20 +39,38 @@ class ShardGroup:
             return cls(dist.get_rank(group), dist.get_world_size(group), group)
         return cls()
 
+    def _host_staged(self, t: torch.Tensor) -> bool:
+        """gloo (CPU tests, several ranks sharing one GPU) moves device tensors through the host."""
+        import torch.distributed as dist
+
+        return t.device.type == "cuda" and dist.get_backend(self.group) == "gloo"
+
     def all_gather(self, shard: torch.Tensor) -> torch.Tensor:
         """Concatenate the equal-size shards of every rank (RCCL all-gather over xGMI)."""
         if self.world == 1:
             return shard
         import torch.distributed as dist
 
+        if self._host_staged(shard):
+            return self.__class__.all_gather(self, shard.cpu()).to(shard.device)
         out = torch.empty(self.world * shard.numel(), dtype=shard.dtype, device=shard.device)
+        if shard.device.type == "cpu" and dist.get_backend(self.group) == "gloo":
+            parts = list(out.chunk(self.world))
+            dist.all_gather(parts, shard.contiguous(), group=self.group)
+            return torch.cat(parts)
         dist.all_gather_into_tensor(out, shard.contiguous(), group=self.group)
         return out
 
     def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over ranks (RCCL all-reduce; the K per-client partial norms of q-FedAvg)."""
         if self.world == 1:
             return t
         import torch.distributed as dist
 
+        if self._host_staged(t):
+            h = t.cpu()
+            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+            t.copy_(h)
+            return t
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t

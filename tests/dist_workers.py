@@ -1,0 +1,94 @@
+"""Worker functions for the multi-process tests (spawned; importable module)."""
+import os
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def _init(rank, world, port):
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+
+
+def cpu_shard_worker(rank, world, port, name):
+    """Sharded layout + collectives on CPU: every rank reduces its slice with the oracle arithmetic;
+    the all-gather reassembles exactly the unsharded result, and the all-reduced per-client partial
+    squared norms equal the unsharded ones (the q-FedAvg exchange)."""
+    from fedscale_amd.bucket import BucketLayout
+    from fedscale_amd.state import ShardGroup
+    from oracle.cpu_reference import fedavg_flat
+    from tests.golden_io import Scenario
+
+    _init(rank, world, port)
+    try:
+        sc = Scenario(name)
+        dtypes = [getattr(torch, d) for d in sc.meta["dtypes"]]
+        full = BucketLayout(sc.names, sc.meta["shapes"], dtypes)
+        lay = BucketLayout(sc.names, sc.meta["shapes"], dtypes, rank, world)
+        K = sc.meta["rounds"][0]
+        xs = np.zeros((K, lay.ld), np.float32)
+        xf = np.zeros((K, full.ld), np.float32)
+        for k in range(K):
+            upd = full.values_of(sc.client(k))
+            lay.pack_host(upd, xs[k], np.zeros(lay.ldq, np.int64))
+            full.pack_host(upd, xf[k], np.zeros(full.ldq, np.int64))
+        g = ShardGroup(rank, world)
+        shard_mean = fedavg_flat(xs[:, :lay.ld]) if K > 0 else None
+        gathered = g.all_gather(torch.from_numpy(shard_mean)).numpy()
+        np.testing.assert_array_equal(gathered[:full.P_full], fedavg_flat(xf)[:full.P_full])
+        # q-FedAvg partial norms
+        L = xf[0] * np.float32(0.5)
+        Ls = L[lay.p0:lay.p0 + lay.ld] if lay.P else np.zeros(lay.ld, np.float32)
+        Ls = np.pad(Ls, (0, lay.ld - len(Ls)))
+        part = np.array([np.sum(((Ls[:lay.P] - xs[k, :lay.P]) / np.float32(0.05)) ** 2, dtype=np.float64)
+                         for k in range(K)])
+        tot = g.all_reduce_sum(torch.from_numpy(part.copy())).numpy()
+        want = np.array([np.sum(((L[:full.P_full] - xf[k, :full.P_full]) / np.float32(0.05)) ** 2,
+                                dtype=np.float64) for k in range(K)])
+        np.testing.assert_allclose(tot, want, rtol=1e-12)
+    finally:
+        dist.destroy_process_group()
+
+
+def gpu_shard_worker(rank, world, port, name, capacity):
+    """The full device path with the model sharded over `world` ranks (all on cuda:0, gloo for the
+    collectives): per-shard kernels, q-FedAvg norm all-reduce, all-gather reassembly on egress."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator, DeviceAsyncAggregator
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+    from fedscale_amd.state import ShardGroup
+    from tests.golden_io import Scenario, StateDictModule, assert_state_close, assert_state_equal
+
+    _init(rank, world, port)
+    torch.cuda.set_device(0)
+    try:
+        sc = Scenario(name)
+        args = sc.args()
+        opt = (TorchServerOptimizer(args.gradient_policy, args, "cuda:0")
+               if sc.meta.get("optimizer") is not None else None)
+        adapter = TorchModelAdapter(StateDictModule(sc.names, sc.init_state()), optimizer=opt, device="cuda:0",
+                                    shards=ShardGroup(rank, world), staging_capacity=capacity)
+        policy = sc.meta["policy"]
+        if policy == "fedbuff":
+            agg = DeviceAsyncAggregator(adapter, args)
+            agg.round = sc.meta["round"]
+            for k, s in enumerate(sc.meta["staleness"]):
+                agg.client_task_model_version[101 + k] = agg.round - s
+        else:
+            agg = DeviceAggregator(adapter, args)
+        for r, ks in sc.rounds():
+            if policy == "q-fedavg":
+                args.learning_rate = sc.meta["lrs"][r]
+            agg.start_round(len(ks))
+            for res in sc.results(ks, r):
+                agg.on_result(res)
+            got = adapter.get_weights()
+            if policy == "q-fedavg":
+                assert_state_close(got, sc.expected(r), 1e-5, f"{name} rank{rank} r{r}", int_slack=1)
+            elif policy == "fed-yogi":
+                assert_state_close(got, sc.expected(r), 1e-6, f"{name} rank{rank} r{r}")
+            else:
+                assert_state_equal(got, sc.expected(r), f"{name} rank{rank} r{r}")
+    finally:
+        dist.destroy_process_group()

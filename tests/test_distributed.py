@@ -1,0 +1,32 @@
+"""World-size-2 tests of the sharded (one process per GPU) path, gloo backend, 127.0.0.1."""
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+from tests import dist_workers
+from tests.golden_io import scenario_names
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("name", ["fedavg_femnist_cnn_k10", "fedavg_mixed_k7", "fedavg_wide_k64"])
+def test_cpu_sharded_reduction_world2(name):
+    mp.spawn(dist_workers.cpu_shard_worker, args=(2, _port(), name), nprocs=2, join=True)
+
+
+@pytest.mark.parametrize("name", ["fedavg_femnist_cnn_k10"])
+def test_cpu_sharded_reduction_world3(name):
+    mp.spawn(dist_workers.cpu_shard_worker, args=(3, _port(), name), nprocs=3, join=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", [n for n in scenario_names() if n != "kat_linear_225"])
+def test_gpu_sharded_device_path_world2(gpu_device, name):
+    mp.spawn(dist_workers.gpu_shard_worker, args=(2, _port(), name, 2), nprocs=2, join=True)

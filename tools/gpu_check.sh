@@ -46,3 +46,9 @@ if [[ $STAGE == sweep ]]; then
   timeout -k 10 1000 python tools/tune_reduce.py sweep ${SWEEP:-1000:25000000,1000:11191242,1000:12500000,400:50000000,1000:4000000,100:1000000} 3 > $OUT/sweep.log 2>&1 || { tail -20 $OUT/sweep.log; exit 1; }
   cat $OUT/sweep.log
 fi
+if [[ $STAGE == dist ]]; then
+  timeout -k 10 900 python -m pytest tests/test_distributed.py -m gpu -x -q > $OUT/pytest_dist.log 2>&1 || { tail -40 $OUT/pytest_dist.log; exit 1; }
+  tail -3 $OUT/pytest_dist.log
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 1 --clients 100 --params 4000000 --dist-backend gloo --reassemble > $OUT/bench_dist2.log 2>&1 || { tail -30 $OUT/bench_dist2.log; exit 1; }
+  grep '^{' $OUT/bench_dist2.log
+fi
