@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--clients", type=int, default=1000)
     ap.add_argument("--params", type=int, default=25_000_000, help="fp32 parameters per GPU shard")
-    ap.add_argument("--policy", default="fedavg", choices=["fedavg", "fedyogi", "fedbuff"])
+    ap.add_argument("--policy", default="fedavg", choices=["fedavg", "fedyogi", "fedbuff", "qfedavg"])
     ap.add_argument("--reassemble", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample (0 = skip)")
     ap.add_argument("--seed", type=int, default=2024)
@@ -124,12 +124,36 @@ def main():
         a = torch.tensor(np.asarray(s, dtype=np.float32), device=dev)
         denom = float(np.float32(sum(s)))
     gathered = None
+    qf = None
+    if args.policy == "qfedavg":
+        if K > kx.qfed_max_chunk():
+            raise SystemExit(f"--policy qfedavg: K <= {kx.qfed_max_chunk()} per chunk in this bench")
+        rng = np.random.default_rng(args.seed)
+        losses = rng.uniform(0.5, 2.0, size=K)
+        lr, q = 0.05, 1.0
+        qf = dict(last=torch.empty(1, ld, device=dev), delta=torch.zeros(ld, device=dev),
+                  sq=torch.zeros(K, dtype=torch.float64, device=dev), ws=kx.qfed_workspace(K, dev),
+                  hs=torch.zeros(2, device=dev), lr=lr,
+                  alpha=torch.tensor([np.float32(np.float_power(l + 1e-10, q)) for l in losses], device=dev),
+                  c1=torch.tensor([np.float32(q * np.float_power(l + 1e-10, q - 1)) for l in losses], device=dev),
+                  c2=torch.tensor([np.float32((1 / lr) * np.float_power(l + 1e-10, q)) for l in losses], device=dev))
+        synth.fill(qf["last"], 1, P, seed=args.seed + 7919 * rank, scale_noise=0.0)
+        qf["last"] = qf["last"][0]
 
     stream = torch.cuda.current_stream(dev)
 
     def step(ev=None):
         if ev is not None:
             ev[0].record(stream)
+        if qf is not None:  # optimizers.py:73-104: phase 1 (timed as the dominant kernel), hs, phase 2
+            qf["sq"].zero_()
+            kx.qfed_accumulate(x, K, P, last=qf["last"], alpha=qf["alpha"], lr=qf["lr"], delta=qf["delta"],
+                               sqnorm=qf["sq"], workspace=qf["ws"], accumulate=False)
+            if ev is not None:
+                ev[1].record(stream)
+            kx.qfed_hs(qf["sq"], qf["c1"], qf["c2"], K, qf["hs"])
+            kx.qfed_finalize(qf["last"], qf["delta"], qf["hs"], out, P)
+            return
         if yogi is None:
             kx.reduce(x, K, P, out, a=a, denom=denom, finalize=True)
         else:
@@ -175,7 +199,7 @@ def main():
     if rank == 0:
         ms_per_step = wall * 1e3 / args.steps
         value = world * K * args.steps / wall
-        extra = {"fedavg": 0, "fedbuff": 4 * K, "fedyogi": 20 * P}[args.policy]
+        extra = {"fedavg": 0, "fedbuff": 4 * K, "fedyogi": 20 * P, "qfedavg": 4 * P + 8 * K}[args.policy]
         alg_bytes = 4 * K * P + 4 * P + extra  # SURVEY §8d algorithmic bytes per launch (per GPU)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
@@ -188,7 +212,9 @@ def main():
             except Exception:
                 traffic = None
         res = {
-            "metric": "client-updates/s, device-resident FedAvg reduce of K x P fp32 (P per GPU)",
+            "metric": ("client-updates/sec + HBM GB/s, device-resident FedAvg reduce of KxP fp32"
+                       if args.policy == "fedavg" else
+                       f"client-updates/sec + HBM GB/s, device-resident {args.policy} round of KxP fp32"),
             "value": value, "unit": "client-updates/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32",
@@ -200,8 +226,10 @@ def main():
             "kernel_ms": kern_ms,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "k_reduce (fa_reduce FA_FINALIZE)" if args.policy != "fedyogi" else
-                         "k_reduce EPI_YOGI (fa_reduce_yogi)",
+                         "kernel": {"fedavg": "k_reduce (fa_reduce FA_FINALIZE)",
+                                    "fedbuff": "k_reduce weighted (fa_reduce FA_FINALIZE)",
+                                    "fedyogi": "k_reduce EPI_YOGI (fa_reduce_yogi)",
+                                    "qfedavg": "k_qfed_accum + k_qfed_gather (fa_qfed_accumulate)"}[args.policy],
                          "alg_bytes_per_launch": alg_bytes},
         }
         if reassembly_ms is not None:

@@ -32,6 +32,7 @@ if [[ $STAGE == pmc ]]; then
   ARGS="--steps 3 --warmup 1 --cpu-seconds 0"
   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $ROOT/bench.py $ARGS > $OUT/pmc_fetch.log 2>&1 || { tail -20 $OUT/pmc_fetch.log; exit 1; }
   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $ROOT/bench.py $ARGS > $OUT/pmc_write.log 2>&1 || { tail -20 $OUT/pmc_write.log; exit 1; }
+  rm -f profiles/pmc_traffic.json
   python tools/pmc_parse.py $OUT/pmc_fetch $OUT/pmc_write fedavg_k1000_p25000000 $((4*1000*25000000 + 4*25000000)) && cp profiles/pmc_traffic.json $OUT/
 fi
 if [[ $STAGE == tune ]]; then
@@ -51,4 +52,14 @@ if [[ $STAGE == dist ]]; then
   tail -3 $OUT/pytest_dist.log
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 1 --clients 100 --params 4000000 --dist-backend gloo --reassemble > $OUT/bench_dist2.log 2>&1 || { tail -30 $OUT/bench_dist2.log; exit 1; }
   grep '^{' $OUT/bench_dist2.log
+fi
+if [[ $STAGE == ingress ]]; then
+  timeout -k 10 600 python tools/ingress_bench.py 200 3 resnet18 > $OUT/ingress.log 2>&1 || { tail -30 $OUT/ingress.log; exit 1; }
+  grep '^{' $OUT/ingress.log
+fi
+if [[ $STAGE == policies ]]; then
+  for pol in ${POLS:-fedbuff fedyogi qfedavg}; do
+    timeout -k 10 300 python bench.py --policy $pol --steps 10 --cpu-seconds 0 > $OUT/bench_$pol.log 2>&1 || { tail -20 $OUT/bench_$pol.log; exit 1; }
+    grep '^{' $OUT/bench_$pol.log
+  done
 fi

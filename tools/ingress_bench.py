@@ -1,0 +1,71 @@
+"""Host-ingress-inclusive aggregation rate: client updates arrive as dicts of numpy
+arrays in pageable host memory (what pickle.loads of the gRPC payload yields, aggregator.py:704 /
+torch_client.py:76-78), pass through DeviceAggregator.update_weight_aggregation (pack into pinned host
+memory -> async H2D -> chunked in-order reduction), and the round ends with get_weights() (D2H egress,
+torch_model_adapter.py:41-47).
+
+usage: python tools/ingress_bench.py [K] [rounds] [layout=resnet18|femnist]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    K = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
+    which = sys.argv[3] if len(sys.argv) > 3 else "resnet18"
+    from fedscale_amd import synth
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    names, shapes, dtypes = synth.resnet18_layout() if which == "resnet18" else synth.femnist_cnn_layout()
+    model = synth.LayoutModule(names, shapes, dtypes)
+    adapter = TorchModelAdapter(model, device="cuda:0")
+    agg = DeviceAggregator(adapter)
+    rng = np.random.default_rng(0)
+    pool = []
+    for i in range(8):
+        d = {}
+        for n, t in model.state_dict().items():
+            if t.dtype == torch.int64:
+                d[n] = np.array(5 + i, dtype=np.int64).reshape(t.shape)
+            else:
+                d[n] = (t.numpy() + rng.standard_normal(t.shape, dtype=np.float32) * np.float32(0.01))
+        pool.append(d)
+    P = adapter.layout.P_full
+    res = []
+    for r in range(rounds + 1):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        agg.start_round(K)
+        t_ing = 0.0
+        for k in range(K):
+            agg.on_result({"client_id": k, "update_weight": pool[k % 8], "moving_loss": 1.0})
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        w = adapter.get_weights()
+        t2 = time.perf_counter()
+        if r > 0:  # first round warms up allocations
+            res.append((t1 - t0, t2 - t1))
+    t_round = float(np.median([a for a, _ in res]))
+    t_egress = float(np.median([b for _, b in res]))
+    out = {"layout": which, "K": K, "P": P, "round_s_incl_h2d": t_round, "egress_d2h_s": t_egress,
+           "client_updates_per_s_incl_h2d": K / t_round,
+           "client_updates_per_s_incl_h2d_d2h": K / (t_round + t_egress),
+           "ingress_GBps": 4 * K * P / t_round / 1e9,
+           "staging_capacity": adapter.staging.capacity}
+    print(json.dumps(out))
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    json.dump(out, open(os.path.join(ROOT, "gpurun_out", f"ingress_{which}_k{K}.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
