@@ -131,6 +131,12 @@ class TorchModelAdapter(ModelAdapterBase):
             self._module_version = self._version
         return self.model
 
+    def __reduce__(self):
+        """Pickle like the reference adapter (model + optimizer): the aggregator sizes simulated model
+        transfers with ``sys.getsizeof(pickle.dumps(self.model_wrapper))`` (aggregator.py:422-424), so the
+        device buffers must not inflate it.  Unpickling rebuilds the HBM state on the current device."""
+        return (self.__class__, (self.get_model(), self.optimizer))
+
     # ---- device fast path -----------------------------------------------------------------------
     def begin_round(self, K: int, policy: str, capacity: Optional[int] = None) -> DeviceRound:
         cap = capacity or self.staging_capacity

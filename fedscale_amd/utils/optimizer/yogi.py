@@ -36,6 +36,25 @@ class YoGi:
         self.m = self.v = self.ms = self.vs = None
         self.initialized = False  # becomes True after the first step (yogi.py:17-19 lazy init)
 
+    def __getstate__(self):
+        """Pickle the hyper-parameters and (host copies of) the m/v state, like the reference object."""
+        st = {k: self.__dict__[k] for k in ("eta", "tau", "beta", "beta2", "initialized")}
+        st["_layout_args"] = None
+        st["_state"] = None
+        if self.layout is not None:
+            L = self.layout
+            st["_layout_args"] = (L.names, [e.shape for e in L.entries], [e.dtype for e in L.entries], L.rank, L.world)
+            st["_state"] = tuple(t.cpu() for t in (self.m, self.v, self.ms, self.vs))
+        return st
+
+    def __setstate__(self, st):
+        self.__init__(st["eta"], st["tau"], st["beta"], st["beta2"])
+        if st.get("_layout_args") is not None:
+            self.bind(BucketLayout(*st["_layout_args"]), torch.device("cuda", torch.cuda.current_device()))
+            for dst, src in zip((self.m, self.v, self.ms, self.vs), st["_state"]):
+                dst.copy_(src)
+        self.initialized = st["initialized"]
+
     # ---- state ----------------------------------------------------------------------------------
     def bind(self, layout: BucketLayout, device):
         """Allocate m/v for ``layout`` (idempotent for the same layout)."""

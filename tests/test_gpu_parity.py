@@ -261,3 +261,22 @@ def test_errors_are_loud(gpu_device):
         kx.reduce(x.cpu(), 2, 64, out)
     with pytest.raises(FedAggError):  # the C ABI itself rejects a misaligned pointer
         call("fa_reduce", x.data_ptr() + 4, 64, 2, 60, None, None, out.data_ptr(), 1.0, 2, None)
+
+
+def test_pickled_adapter_size_matches_reference(gpu_device):
+    """aggregator.py:422-424 sizes simulated transfers from pickle.dumps(model_wrapper)."""
+    import pickle
+
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+    from oracle.cpu_reference import OracleModelAdapter, OracleServerOptimizer
+
+    sc = Scenario("fedyogi_wide_3rounds")
+    args = sc.args()
+    net = torch.nn.Sequential(torch.nn.Linear(300, 200), torch.nn.BatchNorm1d(200))
+    ours = TorchModelAdapter(net, optimizer=TorchServerOptimizer("fed-yogi", args, None))
+    ref = OracleModelAdapter(net, OracleServerOptimizer("fed-yogi", args))
+    a, b = len(pickle.dumps(ours)), len(pickle.dumps(ref))
+    assert abs(a - b) < 0.02 * b, (a, b)
+    back = pickle.loads(pickle.dumps(ours))
+    assert_state_equal(back.get_weights(), ours.get_weights(), "unpickled adapter")
