@@ -373,14 +373,25 @@ extern "C" int fa_yogi_step(const float* cur, const float* last, float* m, float
 // ------------------------------------------------------------------------------------------------
 // q-FedAvg phase 1: delta chain + per-client sum of squares
 // ------------------------------------------------------------------------------------------------
-// Layout: a fixed grid of QF_GRID workgroups (4 waves each) grid-strides over column tiles; the grid
-// size is a constant so the fp64 sum-of-squares order is deterministic across runs and devices.
-// Per tile and client, each lane sums its QF_V*4 squares in fp64, the wave reduces across its 64 lanes
-// (xor butterfly), and lane 0 adds the wave total into an LDS slot [wave][k].  At the end the block
-// writes its 4-wave total per client to workspace[block][k]; k_qfed_gather sums the blocks in order.
-#define QF_V 4
-#define QF_U 2
-#define QF_GRID 1024
+// Layout: a fixed grid of QF_GRID workgroups (4 waves each) grid-strides over column tiles of QF_V KiB
+// per wave; the grid size is a constant so the fp64 sum-of-squares order is deterministic across runs
+// and devices.  Clients are taken in groups of 8: per client each lane sums its QF_V*4 squares in fp64
+// (v[j]); after the group, one "multi-reduce" butterfly (xor 32 / 16 / 8 halve the value set, xor 4 /
+// 2 / 1 finish) leaves lane l with the wave total of client (l >> 3) & 7 — 10 fp64 shuffles per 8
+// clients instead of 48 — and lanes l % 8 == 0 add it into the LDS slot [wave][k].  At the end the
+// block writes its 4-wave total per client to workspace[block][k]; k_qfed_gather sums the blocks in
+// block order.  No atomics: bit-reproducible run to run.
+#ifndef QF_V
+#define QF_V 8
+#endif
+#ifndef QF_U
+#define QF_U 1
+#endif
+#define QF_G 8
+#ifndef QF_GRID
+#define QF_GRID 512  // = 2 workgroups x 256 CUs resident at 2 waves/SIMD (profiles/r01_tune_qfed.log)
+#endif
+
 #define QF_MAXK 1024  // LDS: 4 waves x 1024 clients x 8 B = 32 KiB per workgroup
 
 struct QfArgs {
@@ -390,18 +401,34 @@ struct QfArgs {
   int flags;
   const float* last;
   const float* alpha;
-  float lr;
+  float lr, rlr;  // rlr = RN(1/lr)
+  int fast;       // 0: lr outside [2^-20, 2^20] -> IEEE division for every element
   float* delta;
   double* part;  // [gridDim.x][K]
 };
 
-__device__ __forceinline__ double wave_sum(double s) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  return s;
+// a / b for a runtime-constant divisor b with r = RN(1/b): q = RN(a*r), then one exact-residual
+// correction q + (a - b*q)*r.  Markstein's theorem: r correctly rounded and q within 1 ulp make the
+// corrected quotient the correctly rounded a/b (a quotient has no midpoint cases).  It needs a normal
+// residual and quotient: the host admits only 2^-20 <= |b| <= 2^20 for this path, and per element
+// |a| in [2^-80, 2^80] or a == 0 (fast_div_ok); any other element (denormal, huge, inf, NaN) makes its
+// wave redo that client with the IEEE division (rare, checked once per client with a wave vote).
+__device__ __forceinline__ float fast_div(float a, float b, float r) {
+  const float q = a * r;
+  const float rem = __builtin_fmaf(-q, b, a);
+  return __builtin_fmaf(rem, r, q);
+}
+__device__ __forceinline__ bool fast_div_ok(float a) {
+  const uint32_t m = __builtin_bit_cast(uint32_t, a) & 0x7fffffffu;
+  return (m - 0x17800000u) < (0x67800000u - 0x17800000u) || m == 0u;  // [2^-80, 2^80) or +-0
 }
 
-__global__ __launch_bounds__(256) void k_qfed_accum(QfArgs q) {
+__device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xor(v, m, 64); }
+
+#ifndef QF_MINW
+#define QF_MINW 2
+#endif
+__global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
   __shared__ double sq[4][QF_MAXK];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -423,40 +450,80 @@ __global__ __launch_bounds__(256) void k_qfed_accum(QfArgs q) {
                                                   : f4{0.f, 0.f, 0.f, 0.f};
     }
     const f4* row = xp + c0;
-    int k = 0;
-    for (; k < q.K; k += QF_U) {
-      f4 t[QF_U][QF_V];
+    for (int kg = 0; kg < q.K; kg += QF_G) {
+      double v[QF_G];
 #pragma unroll
-      for (int u = 0; u < QF_U; ++u)
+      for (int jj = 0; jj < QF_G; ++jj) v[jj] = 0.0;
 #pragma unroll
-        for (int j = 0; j < QF_V; ++j)
-          t[u][j] = (ok[j] && k + u < q.K) ? ldnt(row + (int64_t)u * q.ld4 + 64 * j) : f4{0.f, 0.f, 0.f, 0.f};
+      for (int u0 = 0; u0 < QF_G; u0 += QF_U) {
+        f4 t[QF_U][QF_V];
 #pragma unroll
-      for (int u = 0; u < QF_U; ++u) {
-        const int kk = k + u;
-        if (kk >= q.K) break;
-        const float al = q.alpha[kk];
-        const bool first = (kk == 0) && !(q.flags & FA_ACCUMULATE);
-        double acc = 0.0;
+        for (int u = 0; u < QF_U; ++u)
 #pragma unroll
-        for (int j = 0; j < QF_V; ++j) {
-          f4 g;  // ((last - W) * 1.0) / lr, optimizers.py:82-84 (the *1.0 is exact)
-          g.x = __fdiv_rn(L[j].x - t[u][j].x, q.lr);
-          g.y = __fdiv_rn(L[j].y - t[u][j].y, q.lr);
-          g.z = __fdiv_rn(L[j].z - t[u][j].z, q.lr);
-          g.w = __fdiv_rn(L[j].w - t[u][j].w, q.lr);
-          const f4 term = al * g;  // optimizers.py:89,93  float_power(...) * grad  (fp32 product)
-          D[j] = first ? term : D[j] + term;
-          const f4 g2 = g * g;     // torch.square(grad), fp32
-          acc += (double)g2.x;
-          acc += (double)g2.y;
-          acc += (double)g2.z;
-          acc += (double)g2.w;
+          for (int j = 0; j < QF_V; ++j)
+            t[u][j] = (ok[j] && kg + u0 + u < q.K) ? ldnt(row + (int64_t)(u0 + u) * q.ld4 + 64 * j)
+                                                   : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int u = 0; u < QF_U; ++u) {
+          const int kk = kg + u0 + u;
+          if (kk >= q.K) break;  // uniform
+          const float al = q.alpha[kk];
+          const bool first = (kk == 0) && !(q.flags & FA_ACCUMULATE);
+          f4 g[QF_V];
+          bool good = true;
+#pragma unroll
+          for (int j = 0; j < QF_V; ++j) {
+            t[u][j] = L[j] - t[u][j];  // (last - W), optimizers.py:83; the "* 1.0" is exact
+            g[j].x = fast_div(t[u][j].x, q.lr, q.rlr);
+            g[j].y = fast_div(t[u][j].y, q.lr, q.rlr);
+            g[j].z = fast_div(t[u][j].z, q.lr, q.rlr);
+            g[j].w = fast_div(t[u][j].w, q.lr, q.rlr);
+            good = good && fast_div_ok(t[u][j].x) && fast_div_ok(t[u][j].y) && fast_div_ok(t[u][j].z) &&
+                   fast_div_ok(t[u][j].w);
+          }
+          if (!q.fast || !__all(good)) {  // rare: redo this client with the IEEE division
+#pragma unroll
+            for (int j = 0; j < QF_V; ++j) {
+              g[j].x = __fdiv_rn(t[u][j].x, q.lr);
+              g[j].y = __fdiv_rn(t[u][j].y, q.lr);
+              g[j].z = __fdiv_rn(t[u][j].z, q.lr);
+              g[j].w = __fdiv_rn(t[u][j].w, q.lr);
+            }
+          }
+          double acc = 0.0;
+#pragma unroll
+          for (int j = 0; j < QF_V; ++j) {
+            const f4 term = al * g[j];  // optimizers.py:89,93  float_power(...) * grad (fp32 product)
+            D[j] = first ? term : D[j] + term;
+            const f4 g2 = g[j] * g[j];  // torch.square(grad), fp32
+            acc += (double)((g2.x + g2.y) + (g2.z + g2.w));  // 4-term fp32 partial, then fp64
+          }
+          v[u0 + u] = acc;
         }
-        acc = wave_sum(acc);
-        if (lane == 0) sq[wave][kk] += acc;
       }
-      row += QF_U * q.ld4;
+      row += QF_G * q.ld4;
+      // multi-reduce: 8 values per lane -> lane l holds the wave sum of client (l >> 3) & 7
+      double w4[4], w2[2], y;
+      const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double keep = b5 ? v[i + 4] : v[i], send = b5 ? v[i] : v[i + 4];
+        w4[i] = keep + shfl_xor_d(send, 32);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const double keep = b4 ? w4[i + 2] : w4[i], send = b4 ? w4[i] : w4[i + 2];
+        w2[i] = keep + shfl_xor_d(send, 16);
+      }
+      {
+        const double keep = b3 ? w2[1] : w2[0], send = b3 ? w2[0] : w2[1];
+        y = keep + shfl_xor_d(send, 8);
+      }
+      y += shfl_xor_d(y, 4);
+      y += shfl_xor_d(y, 2);
+      y += shfl_xor_d(y, 1);
+      const int jcl = (lane >> 3) & 7;
+      if ((lane & 7) == 0 && kg + jcl < q.K) sq[wave][kg + jcl] += y;
     }
 #pragma unroll
     for (int j = 0; j < QF_V; ++j)
@@ -489,8 +556,11 @@ extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t
   if (!aligned16(x) || !aligned16(last) || !aligned16(delta))
     return fail(FA_E_ARG, "fa_qfed_accumulate: x/last/delta must be 16-byte aligned");
   QfArgs q{};
+  if (!(lr > 1e-30f && lr < 1e30f)) return fail(FA_E_ARG, "fa_qfed_accumulate: lr=%g outside (1e-30, 1e30)", (double)lr);
+
   q.x = x; q.ld4 = ld / 4; q.P4 = (P + 3) / 4; q.K = K; q.flags = flags; q.last = last; q.alpha = alpha;
-  q.lr = lr; q.delta = delta; q.part = (double*)workspace;
+  q.lr = lr; q.rlr = 1.0f / lr; q.delta = delta; q.part = (double*)workspace;
+  q.fast = (lr >= 9.5367432e-07f && lr <= 1048576.f) ? 1 : 0;  // [2^-20, 2^20]
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_qfed_accum, dim3(QF_GRID), dim3(256), 0, st, q);
   int e = check_launch("fa_qfed_accumulate");

@@ -136,6 +136,6 @@ def test_c5_qfedavg_shard_k10000_streamed(gpu_device):
     for k in (0, 4321, K - 1):
         g = (Lfull - synth.host_columns(seed, [k], allc)[0]) / np.float32(lr)
         ref = np.sum((g * g).astype(np.float64))
-        assert abs(sqh[k] - ref) <= 1e-12 * ref
+        assert abs(sqh[k] - ref) <= 1e-9 * ref  # fp32 partials of 4 squares, then fp64
     assert np.all(sqh > 0)
     del x

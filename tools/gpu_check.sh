@@ -63,3 +63,7 @@ if [[ $STAGE == policies ]]; then
     grep '^{' $OUT/bench_$pol.log
   done
 fi
+if [[ $STAGE == tuneqf ]]; then
+  timeout -k 10 900 python tools/tune_qfed.py 1000 25000000 3 > $OUT/tune_qf.log 2>&1 || { tail -20 $OUT/tune_qf.log; exit 1; }
+  cat $OUT/tune_qf.log
+fi
