@@ -146,6 +146,15 @@ int fa_side_qfed_finalize(const int64_t* last, const float* delta_s, const float
 int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uint32_t seed, int32_t k0, float scale_base,
                       float scale_noise, fa_stream_t stream);
 
+/*
+ * Host ingress (no GPU work): copy n host byte ranges srcs[i][0:nbytes[i]] to dst + dst_off[i] with up
+ * to `threads` workers of a persistent pool (used to gather an arriving update's tensors into a pinned
+ * staging row before its H2D copy).  Replaces the per-tensor numpy copies implied by
+ * aggregator.py:494-503's list handling; no reference FFI exists for it.
+ */
+int fa_host_gather(void* dst, const void* const* srcs, const int64_t* dst_off, const int64_t* nbytes, int32_t n,
+                   int32_t threads);
+
 #ifdef __cplusplus
 }
 #endif

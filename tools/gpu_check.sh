@@ -54,7 +54,7 @@ if [[ $STAGE == dist ]]; then
   grep '^{' $OUT/bench_dist2.log
 fi
 if [[ $STAGE == ingress ]]; then
-  timeout -k 10 600 python tools/ingress_bench.py 200 3 resnet18 > $OUT/ingress.log 2>&1 || { tail -30 $OUT/ingress.log; exit 1; }
+  timeout -k 10 600 python tools/ingress_bench.py 200 3 resnet18 ${WORKERS:-1,4,8,16} > $OUT/ingress.log 2>&1 || { tail -30 $OUT/ingress.log; exit 1; }
   grep '^{' $OUT/ingress.log
 fi
 if [[ $STAGE == policies ]]; then

@@ -4,7 +4,7 @@ torch_client.py:76-78), pass through DeviceAggregator.update_weight_aggregation 
 memory -> async H2D -> chunked in-order reduction), and the round ends with get_weights() (D2H egress,
 torch_model_adapter.py:41-47).
 
-usage: python tools/ingress_bench.py [K] [rounds] [layout=resnet18|femnist]
+usage: python tools/ingress_bench.py [K] [rounds] [layout=resnet18|femnist] [pack_workers,...]
 """
 import json
 import os
@@ -22,6 +22,13 @@ def main():
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 200
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     which = sys.argv[3] if len(sys.argv) > 3 else "resnet18"
+    worker_list = [int(w) for w in sys.argv[4].split(",")] if len(sys.argv) > 4 else [None]
+    allout = [run(K, rounds, which, w) for w in worker_list]
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    json.dump(allout, open(os.path.join(ROOT, "gpurun_out", f"ingress_{which}_k{K}.json"), "w"), indent=1)
+
+
+def run(K, rounds, which, workers):
     from fedscale_amd import synth
     from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
     from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
@@ -29,6 +36,11 @@ def main():
     names, shapes, dtypes = synth.resnet18_layout() if which == "resnet18" else synth.femnist_cnn_layout()
     model = synth.LayoutModule(names, shapes, dtypes)
     adapter = TorchModelAdapter(model, device="cuda:0")
+    if workers:
+        adapter.staging = None
+        from fedscale_amd.bucket import ClientStaging
+
+        adapter.staging = ClientStaging(adapter.layout, adapter.device, K, pack_workers=workers)
     agg = DeviceAggregator(adapter)
     rng = np.random.default_rng(0)
     pool = []
@@ -61,10 +73,9 @@ def main():
            "client_updates_per_s_incl_h2d": K / t_round,
            "client_updates_per_s_incl_h2d_d2h": K / (t_round + t_egress),
            "ingress_GBps": 4 * K * P / t_round / 1e9,
-           "staging_capacity": adapter.staging.capacity}
-    print(json.dumps(out))
-    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    json.dump(out, open(os.path.join(ROOT, "gpurun_out", f"ingress_{which}_k{K}.json"), "w"), indent=1)
+           "staging_capacity": adapter.staging.capacity, "pack_workers": adapter.staging.pack_workers}
+    print(json.dumps(out), flush=True)
+    return out
 
 
 if __name__ == "__main__":
