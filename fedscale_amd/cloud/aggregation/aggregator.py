@@ -102,6 +102,37 @@ class DeviceAsyncAggregatorMixin(DeviceAggregatorMixin):
             self._device_round = None
 
 
+class DeviceCohortAggregatorMixin(DeviceAggregatorMixin):
+    """Auxo per-cohort FedAvg (examples/auxo/aggregator.py:451-472), one device round per cohort.
+
+    Every reduction field is a list indexed by ``cohort_id`` (``model_wrapper``, ``model_in_update``,
+    ``tasks_round``, ``model_weights``); each cohort's ``model_wrapper`` is its own device-resident
+    TorchModelAdapter, so cohorts reduce concurrently and independently.  As in the reference,
+    set_weights runs without client_training_results (:472)."""
+
+    def _is_first_result_in_round(self, cohort_id=0):
+        return self.model_in_update[cohort_id] == 1
+
+    def _is_last_result_in_round(self, cohort_id=0):
+        return self.model_in_update[cohort_id] == self.tasks_round[cohort_id]
+
+    def update_weight_aggregation(self, results, cohort_id=0):
+        w = self.model_wrapper[cohort_id]
+        if not isinstance(w, TorchModelAdapter):
+            raise TypeError(f"model_wrapper[{cohort_id}] is {type(w).__name__}; the device path needs "
+                            f"fedscale_amd's TorchModelAdapter")
+        rounds = self.__dict__.setdefault("_device_rounds", {})
+        if self._is_first_result_in_round(cohort_id) or cohort_id not in rounds:
+            rounds[cohort_id] = w.begin_round(self.tasks_round[cohort_id], "fedavg",
+                                              capacity=self.device_round_capacity)
+        rounds[cohort_id].add(results["update_weight"])
+        if self._is_last_result_in_round(cohort_id):
+            K = self.tasks_round[cohort_id]
+            w.apply_round(rounds.pop(cohort_id), float(np.float32(K)), float(K), client_training_results=None,
+                          keep_mean=self.device_keep_mean)
+            self.model_weights[cohort_id] = w.round_mean_weights()
+
+
 class DeviceAggregator(DeviceAggregatorMixin):
     """Standalone holder of the hot-path state contract (for tools, tests and non-FedScale callers)."""
 
@@ -133,3 +164,17 @@ class DeviceAsyncAggregator(DeviceAsyncAggregatorMixin, DeviceAggregator):
         self.round = 0
         self.client_task_model_version = {}
         self.aggregation_denominator = 0
+
+
+class DeviceCohortAggregator(DeviceCohortAggregatorMixin):
+    """Standalone Auxo-style cohort state (tests / tools)."""
+
+    def __init__(self, wrappers, tasks_round):
+        self.model_wrapper = list(wrappers)
+        self.tasks_round = list(tasks_round)
+        self.model_in_update = [0] * len(self.model_wrapper)
+        self.model_weights = [[] for _ in self.model_wrapper]
+
+    def on_result(self, results, cohort_id):
+        self.model_in_update[cohort_id] += 1  # examples/auxo/aggregator.py:307
+        self.update_weight_aggregation(results, cohort_id)

@@ -64,6 +64,7 @@ class TorchModelAdapter(ModelAdapterBase):
         self._f[0].copy_(cur_f)
         self._s[0].copy_(cur_s.to(torch.int64))
         self._version = 0  # bumps on every device-side model update
+        self._host_cache = None
         self._module_version = 0 if _load_from is None else -1
 
     # ---- internal buffers ---------------------------------------------------------------------
@@ -116,13 +117,22 @@ class TorchModelAdapter(ModelAdapterBase):
         ns.copy_(cur_s.to(torch.float32).to(torch.int64))  # float32 -> int64 load truncates (:31-35)
         self._commit_scratch()
 
+    def _host_copy(self):
+        """One D2H (after the shard all-gather) per model version, cached for every egress request of the
+        round (the reference clones + pickles per executor request, aggregator.py:788-804, 902-909)."""
+        if self._host_cache is None or self._host_cache[0] != self._version:
+            L = self.layout
+            full = self.shards.all_gather(self._f[self._cur])
+            f_cpu = torch.empty(L.P_full, dtype=torch.float32, pin_memory=True)
+            f_cpu.copy_(full[:L.P_full])
+            s_cpu = self._s[self._cur][:L.Q].to("cpu")
+            self._host_cache = (self._version, f_cpu, s_cpu)
+        return self._host_cache[1], self._host_cache[2]
+
     def get_weights(self) -> List[torch.Tensor]:
         """torch_model_adapter.py:41-47: cloned CPU tensors in state_dict order (gathers the shards)."""
-        L = self.layout
-        full = self.shards.all_gather(self._f[self._cur])
-        f_cpu = full[:L.P_full].to("cpu")
-        s_cpu = self._s[self._cur][:L.Q].to("cpu")
-        return [t.clone() for t in L.unpack(f_cpu, s_cpu)]
+        f_cpu, s_cpu = self._host_copy()
+        return [t.clone() for t in self.layout.unpack(f_cpu, s_cpu)]
 
     def get_model(self):
         if self._module_version != self._version:

@@ -16,6 +16,7 @@ Reference anchors (paths relative to /root/reference):
 * model adapter set/get ............. fedscale/cloud/internal/torch_model_adapter.py:23-47
 * server optimizer dispatch ......... fedscale/cloud/aggregation/optimizers.py:16-108
 * YoGi .............................. fedscale/utils/optimizer/yogi.py:5-36
+* Auxo per-cohort FedAvg ............ examples/auxo/aggregator.py:451-472
 
 Numerics notes (each reproduced deliberately):
 * accumulation is numpy, fp32, strictly in arrival order, allocating a new array each add;
@@ -220,6 +221,26 @@ class OracleAggregator:
             self.model_weights = fedavg_close(self.model_weights, self.tasks_round)
             self.model_wrapper.set_weights(copy.deepcopy(self.model_weights),
                                            client_training_results=self.client_training_results)
+
+
+class OracleCohortAggregator:
+    """Auxo's per-cohort FedAvg (examples/auxo/aggregator.py:451-472): every reduction field is a list
+    indexed by cohort; set_weights is called without client_training_results (:472)."""
+
+    def __init__(self, wrappers, tasks_round):
+        self.model_wrapper = list(wrappers)
+        self.tasks_round = list(tasks_round)
+        self.model_in_update = [0] * len(self.model_wrapper)
+        self.model_weights = [[] for _ in self.model_wrapper]
+
+    def on_result(self, results, cohort_id):
+        self.model_in_update[cohort_id] += 1  # auxo/aggregator.py:307
+        first = self.model_in_update[cohort_id] == 1
+        last = self.model_in_update[cohort_id] == self.tasks_round[cohort_id]
+        self.model_weights[cohort_id] = fedavg_step(self.model_weights[cohort_id], results["update_weight"], first)
+        if last:
+            self.model_weights[cohort_id] = fedavg_close(self.model_weights[cohort_id], self.tasks_round[cohort_id])
+            self.model_wrapper[cohort_id].set_weights(copy.deepcopy(self.model_weights[cohort_id]))
 
 
 # ------------------------------------------------------------------------------------------------

@@ -407,6 +407,49 @@ def main():
                     losses=all_losses)
         _save(f"qfedavg_{tag}", meta, arrays)
 
+    # 8. Auxo per-cohort FedAvg (examples/auxo/aggregator.py:451-472): two cohorts, interleaved arrivals.
+    #    Auxo's own modules need three more off-path placeholders: nltk (clustering), and its `config`
+    #    module (which would yaml.load a file shipped in the reference; it is never read on this path).
+    import types as _t
+
+    nl = _t.ModuleType("nltk")
+    nlc = _t.ModuleType("nltk.cluster")
+    nlc.KMeansClusterer, nlc.euclidean_distance = object, None
+    nl.cluster = nlc
+    sys.modules.update({"nltk": nl, "nltk.cluster": nlc})
+    cfg = _t.ModuleType("config")
+    cfg.auxo_config = {}
+    sys.modules["config"] = cfg
+    sys.path.insert(0, os.path.join(REF, "examples", "auxo"))
+    from aggregator import AuxoAggregator  # examples/auxo/aggregator.py
+
+    class MockAuxo(AuxoAggregator):
+        def __init__(self, wrappers, K):
+            self.model_weights = [[] for _ in wrappers]
+            self.model_in_update = [0 for _ in wrappers]
+            self.tasks_round = list(K)
+            self.model_wrapper = wrappers
+            self.client_training_results = [[] for _ in wrappers]
+
+    models = [_init_model(MixedNet, 71), _init_model(MixedNet, 72)]
+    wrappers = [TorchModelAdapter(m) for m in models]
+    Ks = [4, 3]
+    order = [0, 1, 0, 0, 1, 1, 0]
+    agg = MockAuxo(wrappers, Ks)
+    meta = _meta_of(models[0])
+    arrays = {}
+    for c, w in enumerate(wrappers):
+        _store_state(arrays, f"init_c{c}", w.get_weights())
+    ups = _client_updates(models[0], len(order), 710)
+    _store_inputs(arrays, ups, meta["names"])
+    for k, c in enumerate(order):
+        agg.model_in_update[c] += 1  # examples/auxo/aggregator.py:307
+        agg.update_weight_aggregation({"client_id": k + 1, "update_weight": ups[k], "moving_loss": 1.0}, c)
+    for c, w in enumerate(wrappers):
+        _store_state(arrays, f"out_c{c}", w.get_weights())
+    meta.update(policy="auxo-cohorts", rounds=[len(order)], cohorts=order, cohort_K=Ks, dict_every=2, optimizer=None)
+    _save("auxo_cohorts_fedavg", meta, arrays)
+
     print("done")
 
 

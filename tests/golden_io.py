@@ -17,8 +17,11 @@ DEFAULT_ARGS = dict(gradient_policy=None, learning_rate=0.05, min_learning_rate=
                     qfed_q=1.0, max_staleness=5)
 
 
-def scenario_names():
-    return sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "*.json")))
+def scenario_names(kind="single"):
+    """kind 'single': one global model per scenario; 'cohorts': Auxo multi-cohort scenarios."""
+    names = sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "*.json")))
+    coh = [n for n in names if n.startswith("auxo_")]
+    return coh if kind == "cohorts" else [n for n in names if n not in coh]
 
 
 class Scenario:
@@ -34,8 +37,12 @@ class Scenario:
     def _tensors(self, prefix):
         return [self.arrays[f"{prefix}/{i}"] for i in range(self.T)]
 
-    def init_state(self):
-        return [torch.from_numpy(np.array(a)) for a in self._tensors("init")]
+    def init_state(self, cohort=None):
+        pre = "init" if cohort is None else f"init_c{cohort}"
+        return [torch.from_numpy(np.array(a)) for a in self._tensors(pre)]
+
+    def expected_cohort(self, c):
+        return self._tensors(f"out_c{c}")
 
     def expected(self, r):
         return self._tensors(f"out/{r}")

@@ -113,3 +113,19 @@ def test_product_never_imports_oracle():
             if f.endswith(".py"):
                 src = open(os.path.join(dirpath, f)).read()
                 assert not re.search(r"^\s*(from|import)\s+oracle", src, re.M), f"{f} imports oracle"
+
+
+@pytest.mark.parametrize("workers", [1, 4, 8])
+def test_native_host_gather(workers):
+    """fa_host_gather (host-only native code, no GPU): pieces land at their offsets, pool path included."""
+    from fedscale_amd.bucket import BucketLayout
+
+    rng = np.random.default_rng(workers)
+    shapes = [(1024, 1025), (3,), (700, 999), (), (5, 7, 11), (2048, 513)]  # > 4 MB in total
+    names = [f"t{i}" for i in range(len(shapes))]
+    vals = [rng.normal(size=s).astype(np.float32) for s in shapes]
+    lay = BucketLayout(names, shapes, [torch.float32] * len(shapes))
+    f = np.full(lay.ld, -1, np.float32)
+    lay.pack_host(vals, f, np.zeros(1, np.int64), workers=workers)
+    np.testing.assert_array_equal(f[:lay.P], np.concatenate([v.reshape(-1) for v in vals]))
+    assert np.all(f[lay.P:] == -1)

@@ -309,3 +309,21 @@ def test_qfed_division_is_correctly_rounded(gpu_device, lr):
     same = (got == want) | (np.isnan(got) & np.isnan(want))
     assert same.all(), f"{(~same).sum()} mismatches, e.g. a={a[~same][:3]} got={got[~same][:3]} want={want[~same][:3]}"
     assert (np.signbit(got) == np.signbit(want))[~np.isnan(want)].all()
+
+
+@pytest.mark.parametrize("capacity", [None, 2])
+@pytest.mark.parametrize("name", scenario_names("cohorts"))
+def test_auxo_cohorts_match_reference_fixture(gpu_device, name, capacity):
+    """Two cohorts with interleaved arrivals, each reduced on its own device adapter (bit-exact)."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceCohortAggregator
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    sc = Scenario(name)
+    n = len(sc.meta["cohort_K"])
+    wrappers = [TorchModelAdapter(StateDictModule(sc.names, sc.init_state(c)), device="cuda:0",
+                                  staging_capacity=capacity) for c in range(n)]
+    agg = DeviceCohortAggregator(wrappers, sc.meta["cohort_K"])
+    for k, c in enumerate(sc.meta["cohorts"]):
+        agg.on_result({"client_id": k + 1, "update_weight": sc.client(k), "moving_loss": 1.0}, c)
+    for c, w in enumerate(wrappers):
+        assert_state_equal(w.get_weights(), sc.expected_cohort(c), f"{name} cohort {c}")

@@ -33,3 +33,16 @@ def test_oracle_matches_reference_fixture(name):
             m, v = sc.yogi_state(r)
             assert_state_equal(opt.gradient_controller.m_t, m, f"{name} m round {r}")
             assert_state_equal(opt.gradient_controller.v_t, v, f"{name} v round {r}")
+
+
+@pytest.mark.parametrize("name", scenario_names("cohorts"))
+def test_oracle_matches_auxo_cohort_fixture(name):
+    from oracle.cpu_reference import OracleCohortAggregator
+
+    sc = Scenario(name)
+    wrappers = [OracleModelAdapter(OracleModel(sc.names, sc.init_state(c))) for c in range(len(sc.meta["cohort_K"]))]
+    agg = OracleCohortAggregator(wrappers, sc.meta["cohort_K"])
+    for k, c in enumerate(sc.meta["cohorts"]):
+        agg.on_result({"client_id": k + 1, "update_weight": sc.client(k), "moving_loss": 1.0}, c)
+    for c, w in enumerate(wrappers):
+        assert_state_equal(w.get_weights(), sc.expected_cohort(c), f"{name} cohort {c}")
