@@ -24,11 +24,13 @@ def main():
     which = sys.argv[3] if len(sys.argv) > 3 else "resnet18"
     worker_list = [int(w) for w in sys.argv[4].split(",")] if len(sys.argv) > 4 else [None]
     allout = [run(K, rounds, which, w) for w in worker_list]
+    # full ingress from the executor's pickled payload (aggregator.py:704 deserialize_response)
+    allout.append(run(K, rounds, which, None, loader="pickle"))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(allout, open(os.path.join(ROOT, "gpurun_out", f"ingress_{which}_k{K}.json"), "w"), indent=1)
 
 
-def run(K, rounds, which, workers):
+def run(K, rounds, which, workers, loader=None):
     from fedscale_amd import synth
     from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
     from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
@@ -53,6 +55,16 @@ def run(K, rounds, which, workers):
                 d[n] = (t.numpy() + rng.standard_normal(t.shape, dtype=np.float32) * np.float32(0.01))
         pool.append(d)
     P = adapter.layout.P_full
+    payloads = None
+    if loader is not None:
+        import pickle
+
+        payloads = [pickle.dumps({"client_id": i, "update_weight": d, "moving_loss": 1.0}) for i, d in enumerate(pool)]
+        load = pickle.loads
+        t0 = time.perf_counter()
+        for r in range(16):
+            load(payloads[r % 8])
+        t_load = (time.perf_counter() - t0) / 16
     res = []
     for r in range(rounds + 1):
         torch.cuda.synchronize()
@@ -60,7 +72,10 @@ def run(K, rounds, which, workers):
         agg.start_round(K)
         t_ing = 0.0
         for k in range(K):
-            agg.on_result({"client_id": k, "update_weight": pool[k % 8], "moving_loss": 1.0})
+            if payloads is not None:
+                agg.on_result(load(payloads[k % 8]))
+            else:
+                agg.on_result({"client_id": k, "update_weight": pool[k % 8], "moving_loss": 1.0})
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         w = adapter.get_weights()
@@ -73,7 +88,8 @@ def run(K, rounds, which, workers):
            "client_updates_per_s_incl_h2d": K / t_round,
            "client_updates_per_s_incl_h2d_d2h": K / (t_round + t_egress),
            "ingress_GBps": 4 * K * P / t_round / 1e9,
-           "staging_capacity": adapter.staging.capacity, "pack_workers": adapter.staging.pack_workers}
+           "staging_capacity": adapter.staging.capacity, "pack_workers": adapter.staging.pack_workers,
+           "from_payload": loader, "loads_ms_per_update": (t_load * 1e3 if loader else None)}
     print(json.dumps(out), flush=True)
     return out
 
