@@ -806,6 +806,54 @@ extern "C" int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uin
 }
 
 // ------------------------------------------------------------------------------------------------
+// HeteroFL sub-model combination (examples/heterofl/customized_aggregator.py:78-119)
+// ------------------------------------------------------------------------------------------------
+// A client at model rate r uploads, for every tensor of shape (O, I, S...), the prefix box
+// [0:o) x [0:i) x S (examples/heterofl/customized_fllibs.py:25-70 only ever builds prefix index sets).
+// Per global element, the reference sums the covering clients' values in client order into an fp32
+// zero, counts them, and replaces the element by sum / count where count > 0.  One thread per element;
+// a workgroup covers HB_ELEMS elements of ONE tensor, so the per-client box descriptors are uniform
+// (scalar loads) and a client's covered elements are contiguous runs of its upload.
+#define HB_ELEMS 1024
+
+__global__ __launch_bounds__(256) void k_prefix_box(const float* __restrict__ xs, const int64_t* __restrict__ desc,
+                                                    int K, int T, const int64_t* __restrict__ tens,
+                                                    const int32_t* __restrict__ ck_t,
+                                                    const int64_t* __restrict__ ck_first, float* glob) {
+  const int c = blockIdx.x;
+  const int k = ck_t[c];
+  const int64_t goff = tens[4 * k], I = tens[4 * k + 2], S = tens[4 * k + 3];
+  const int64_t n = tens[4 * k + 1] * I * S;
+  for (int j = 0; j < HB_ELEMS / 256; ++j) {
+    const int64_t e = ck_first[c] + j * 256 + threadIdx.x;
+    if (e >= n) break;
+    const int64_t o = e / (I * S), r = e - o * I * S, i = r / S, s = r - i * S;
+    float acc = 0.f;  // tmp_v = v.new_zeros(..., dtype=torch.float32)
+    int cnt = 0;
+    for (int m = 0; m < K; ++m) {
+      const int64_t* d = desc + 3 * ((int64_t)m * T + k);
+      if (o < d[1] && i < d[2]) {
+        acc = acc + xs[d[0] + (o * d[2] + i) * S + s];  // tmp_v[idx] += local_parameters[k]
+        ++cnt;                                          // count[k][idx] += 1
+      }
+    }
+    if (cnt > 0) glob[goff + e] = __fdiv_rn(acc, (float)cnt);  // tmp_v[count>0].div_(count[count>0])
+  }
+}
+
+extern "C" int fa_prefix_box_combine(const float* xs, const int64_t* desc, int32_t K, const int64_t* tensors,
+                                     int32_t T, const int32_t* chunk_tensor, const int64_t* chunk_first,
+                                     int32_t nchunks, float* global, fa_stream_t stream) {
+  if (K < 0 || T < 0 || nchunks < 0) return fail(FA_E_ARG, "fa_prefix_box_combine: negative sizes");
+  if (nchunks == 0 || K == 0) return FA_OK;
+  if (!xs || !desc || !tensors || !chunk_tensor || !chunk_first || !global)
+    return fail(FA_E_ARG, "fa_prefix_box_combine: NULL pointer");
+  hipLaunchKernelGGL(k_prefix_box, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, xs, desc, (int)K, (int)T, tensors,
+                     chunk_tensor, chunk_first, global);
+  return check_launch("fa_prefix_box_combine");
+}
+
+// ------------------------------------------------------------------------------------------------
 // host ingress: multi-threaded gather of a client update's tensors into a pinned staging row
 // ------------------------------------------------------------------------------------------------
 // One call per arriving update (the reference's dict of numpy arrays, torch_client.py:76-78): the byte

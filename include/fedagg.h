@@ -147,6 +147,19 @@ int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uint32_t seed,
                       float scale_noise, fa_stream_t stream);
 
 /*
+ * HeteroFL sub-model combination: replaces Customized_Aggregator.combine_models,
+ * examples/heterofl/customized_aggregator.py:78-119 (index sets from customized_fllibs.py:25-70 are
+ * prefixes, so client m's upload of tensor k is the box [0:o) x [0:i) x S of the global (O, I, S)).
+ *   xs       concatenated client uploads (fp32), desc[(m*T + k)*3 + {0,1,2}] = {offset in xs, o, i}
+ *   tensors  [T][4] = {offset in global, O, I, S};  chunks: workgroup c covers elements
+ *            [chunk_first[c], chunk_first[c] + 1024) of tensor chunk_tensor[c]
+ * global[e] <- (sum over covering clients, client order, fp32 from 0) / fp32(count) where count > 0.
+ */
+int fa_prefix_box_combine(const float* xs, const int64_t* desc, int32_t K, const int64_t* tensors, int32_t T,
+                          const int32_t* chunk_tensor, const int64_t* chunk_first, int32_t nchunks, float* global,
+                          fa_stream_t stream);
+
+/*
  * Host ingress (no GPU work): copy n host byte ranges srcs[i][0:nbytes[i]] to dst + dst_off[i] with up
  * to `threads` workers of a persistent pool (used to gather an arriving update's tensors into a pinned
  * staging row before its H2D copy).  Replaces the per-tensor numpy copies implied by

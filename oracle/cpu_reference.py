@@ -17,6 +17,7 @@ Reference anchors (paths relative to /root/reference):
 * server optimizer dispatch ......... fedscale/cloud/aggregation/optimizers.py:16-108
 * YoGi .............................. fedscale/utils/optimizer/yogi.py:5-36
 * Auxo per-cohort FedAvg ............ examples/auxo/aggregator.py:451-472
+* HeteroFL combine_models ........... examples/heterofl/customized_aggregator.py:78-119
 
 Numerics notes (each reproduced deliberately):
 * accumulation is numpy, fp32, strictly in arrival order, allocating a new array each add;
@@ -241,6 +242,23 @@ class OracleCohortAggregator:
         if last:
             self.model_weights[cohort_id] = fedavg_close(self.model_weights[cohort_id], self.tasks_round[cohort_id])
             self.model_wrapper[cohort_id].set_weights(copy.deepcopy(self.model_weights[cohort_id]))
+
+
+def heterofl_combine(global_sd, local_states):
+    """Restatement of Customized_Aggregator.combine_models (examples/heterofl/customized_aggregator.py:78-119)
+    for prefix index sets (customized_fllibs.py:25-70 builds only prefixes): per tensor an fp32 zero sum
+    and count, clients scatter-added in order, then sum/count where count > 0 (in place on global_sd)."""
+    for name, v in global_sd.items():
+        tmp = torch.zeros(v.shape, dtype=torch.float32)
+        cnt = torch.zeros(v.shape, dtype=torch.float32)
+        for loc in local_states:
+            lv = torch.as_tensor(np.asarray(loc[name]))
+            box = tuple(slice(0, n) for n in lv.shape[:2])
+            tmp[box] += lv
+            cnt[box] += 1
+        mask = cnt > 0
+        tmp[mask] = tmp[mask].div_(cnt[mask])
+        v[mask] = tmp[mask].to(v.dtype)
 
 
 # ------------------------------------------------------------------------------------------------

@@ -450,6 +450,58 @@ def main():
     meta.update(policy="auxo-cohorts", rounds=[len(order)], cohorts=order, cohort_K=Ks, dict_every=2, optimizer=None)
     _save("auxo_cohorts_fedavg", meta, arrays)
 
+    # 9. HeteroFL sub-model combination (examples/heterofl/customized_aggregator.py:78-119): clients at
+    #    model rates 1 / 0.5 / 0.25 / 0.125 upload prefix slices of every tensor; the global model takes the
+    #    per-element mean over the clients that cover it.  The example's `config` module would open its
+    #    YAML with a non-safe loader: a placeholder reads the same config.yml with yaml.safe_load (and
+    #    shrinks resnet_hidden_size so the fixture stays small); its outdated logger import gets a placeholder.
+    import yaml
+
+    hdir = os.path.join(REF, "examples", "heterofl")
+    hcfg = _t.ModuleType("config")
+    with open(os.path.join(hdir, "config.yml")) as f:
+        hcfg.cfg = yaml.safe_load(f)
+    hcfg.cfg["resnet_hidden_size"] = [4, 8, 16, 32]
+    sys.modules["config"] = hcfg
+    sys.modules["fedscale.cloud.logger.aggregation_logging"] = _t.ModuleType("fedscale.cloud.logger.aggregation_logging")
+    sys.path.insert(0, hdir)
+    for m in ("aggregator", "client_manager", "resource_manager"):
+        sys.modules.pop(m, None)  # auxo's same-named modules
+    import customized_fllibs
+    import resnet_heterofl
+    from customized_aggregator import Customized_Aggregator
+
+    class MockHetero(Customized_Aggregator):
+        def __init__(self, model, results):
+            self.model = model
+            self.param_idx = {}
+            self.client_training_results = results
+
+    torch.manual_seed(81)
+    gmodel = resnet_heterofl.resnet18(model_rate=1, track=False)
+    with torch.no_grad():
+        g = torch.Generator().manual_seed(82)
+        for t in gmodel.state_dict().values():
+            t.copy_((torch.randn(t.shape, generator=g) * 0.05).half().float())
+    rates = [1, 0.5, 0.25, 0.125, 1, 0.5, 0.0625]
+    rng = np.random.default_rng(83)
+    results = []
+    for r in rates:
+        local = customized_fllibs.split_model(gmodel, r)
+        for k in local:
+            local[k] = torch.from_numpy(_f16_exact(rng, tuple(local[k].shape), 0.01, loc=local[k].numpy()))
+        results.append({"model_rate": r, "local_parameters": local})
+    meta = _meta_of(gmodel)
+    arrays = {}
+    _store_state(arrays, "init", list(gmodel.state_dict().values()))
+    for m, res in enumerate(results):
+        for i, v in enumerate(res["local_parameters"].values()):
+            arrays[f"client/{m}/{i}"] = _compact(v.numpy())
+    MockHetero(gmodel, results).combine_models()
+    _store_state(arrays, "out/0", list(gmodel.state_dict().values()))
+    meta.update(policy="heterofl", rounds=[len(rates)], rates=rates, optimizer=None)
+    _save("heterofl_resnet18_small", meta, arrays)
+
     print("done")
 
 

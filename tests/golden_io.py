@@ -21,7 +21,12 @@ def scenario_names(kind="single"):
     """kind 'single': one global model per scenario; 'cohorts': Auxo multi-cohort scenarios."""
     names = sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "*.json")))
     coh = [n for n in names if n.startswith("auxo_")]
-    return coh if kind == "cohorts" else [n for n in names if n not in coh]
+    het = [n for n in names if n.startswith("heterofl_")]
+    if kind == "cohorts":
+        return coh
+    if kind == "heterofl":
+        return het
+    return [n for n in names if n not in coh and n not in het]
 
 
 class Scenario:
@@ -40,6 +45,14 @@ class Scenario:
     def init_state(self, cohort=None):
         pre = "init" if cohort is None else f"init_c{cohort}"
         return [torch.from_numpy(np.array(a)) for a in self._tensors(pre)]
+
+    def hetero_locals(self):
+        """[per client: {name: local prefix-box array}] of a heterofl fixture."""
+        out = []
+        for m in range(len(self.meta["rates"])):
+            vals = [a.astype(np.float32) if a.dtype == np.float16 else a for a in self._tensors(f"client/{m}")]
+            out.append(dict(zip(self.names, vals)))
+        return out
 
     def expected_cohort(self, c):
         return self._tensors(f"out_c{c}")

@@ -327,3 +327,23 @@ def test_auxo_cohorts_match_reference_fixture(gpu_device, name, capacity):
         agg.on_result({"client_id": k + 1, "update_weight": sc.client(k), "moving_loss": 1.0}, c)
     for c, w in enumerate(wrappers):
         assert_state_equal(w.get_weights(), sc.expected_cohort(c), f"{name} cohort {c}")
+
+
+@pytest.mark.parametrize("name", scenario_names("heterofl"))
+def test_heterofl_combine_matches_reference_fixture(gpu_device, name):
+    """HeteroFL sub-model combination (examples/heterofl/customized_aggregator.py:78-119), bit-exact."""
+    from collections import OrderedDict
+
+    from fedscale_amd.cloud.aggregation.heterofl import DeviceHeteroFLMixin
+
+    sc = Scenario(name)
+
+    class Agg(DeviceHeteroFLMixin):
+        pass
+
+    agg = Agg()
+    agg.model = StateDictModule(sc.names, sc.init_state())
+    agg.client_training_results = [{"model_rate": r, "local_parameters": loc}
+                                   for r, loc in zip(sc.meta["rates"], sc.hetero_locals())]
+    agg.combine_models()
+    assert_state_equal(list(agg.model.state_dict().values()), sc.expected(0), name)

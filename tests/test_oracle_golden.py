@@ -46,3 +46,15 @@ def test_oracle_matches_auxo_cohort_fixture(name):
         agg.on_result({"client_id": k + 1, "update_weight": sc.client(k), "moving_loss": 1.0}, c)
     for c, w in enumerate(wrappers):
         assert_state_equal(w.get_weights(), sc.expected_cohort(c), f"{name} cohort {c}")
+
+
+@pytest.mark.parametrize("name", scenario_names("heterofl"))
+def test_oracle_matches_heterofl_fixture(name):
+    from collections import OrderedDict
+
+    from oracle.cpu_reference import heterofl_combine
+
+    sc = Scenario(name)
+    sd = OrderedDict(zip(sc.names, sc.init_state()))
+    heterofl_combine(sd, sc.hetero_locals())
+    assert_state_equal(list(sd.values()), sc.expected(0), name)
