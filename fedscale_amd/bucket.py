@@ -181,6 +181,7 @@ class ClientStaging:
         self.pack_workers = pack_workers or default_pack_workers()
         self.device = torch.device(device)
         self.capacity = int(capacity)
+        self.generation = 0  # bumped by every DeviceRound that takes the slots over
         self.x = torch.zeros(self.capacity, layout.ld, dtype=torch.float32, device=self.device)
         self.xi = torch.zeros(self.capacity, layout.ldq, dtype=torch.int64, device=self.device)
         self._ring = []

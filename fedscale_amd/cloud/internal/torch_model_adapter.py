@@ -171,6 +171,7 @@ class TorchModelAdapter(ModelAdapterBase):
                 raise RuntimeError("a q-FedAvg round needs the q-fedavg server optimizer")
             rnd.finalize_qfed(out=out_f, model_side=out_s, sqnorm_allreduce=self._sqnorm_allreduce())
             self._mean_valid = False
+            self._mean_round = rnd  # the mean can still be recomputed lazily from the staged updates
         elif mode == "fed-yogi":
             y = opt.gradient_controller
             y.bind(L, self.device)
@@ -199,9 +200,17 @@ class TorchModelAdapter(ModelAdapterBase):
         return LazyWeights(self)
 
     def _fetch_mean(self) -> list:
+        rnd = getattr(self, "_mean_round", None)
+        if not self._mean_valid and rnd is not None:
+            L = self.layout
+            mean_f = torch.zeros(L.ld, dtype=torch.float32, device=self.device)
+            if rnd.mean_from_staging(mean_f, self._mean_s):
+                self._mean_f, self._mean_valid = mean_f, True
+            self._mean_round = None
         if not self._mean_valid or self._mean_f is None:
-            raise RuntimeError("the FedAvg mean of this round was not materialised on the device "
-                               "(q-FedAvg discards it; fed-yogi keeps it unless keep_mean=False)")
+            raise RuntimeError("the FedAvg mean of this round is not available on the device: a q-FedAvg "
+                               "round keeps it only while all K updates are still staged (one chunk), and "
+                               "fed-yogi keeps it unless keep_mean=False")
         L = self.layout
         full = self.shards.all_gather(self._mean_f[:L.ld])
         f_cpu = full[:L.P_full].to("cpu").numpy()

@@ -51,6 +51,8 @@ class DeviceRound:
             cap = capacity or default_capacity(layout, K, self.device)
             self.staging = ClientStaging(layout, self.device, min(cap, K))
         self.cap = min(self.staging.capacity, capacity or self.staging.capacity)
+        self.staging.generation += 1  # a new round takes the staging slots over
+        self.generation = self.staging.generation
         self.n = 0  # results received
         self.slot = 0  # staged in the current chunk
         self.chunks_done = 0
@@ -161,6 +163,19 @@ class DeviceRound:
         mode = 0 if self.policy == "fedavg" else 1
         kx.side_accumulate(st.xi, n, L.Q, mode, w=a64, acc_i=self.acc_i, acc_d=self.acc_d, accumulate=not first)
         kx.side_close(L.Q, mode, denom64, acc_i=self.acc_i, acc_d=self.acc_d, cur=cur_side, model=model_side)
+
+    def mean_from_staging(self, out: torch.Tensor, cur_side: torch.Tensor) -> bool:
+        """The plain FedAvg mean of this round (aggregator.py:497-507), recomputed from the staged updates
+        when they are all still resident (q-FedAvg rounds do not need it, but the reference keeps it in
+        ``Aggregator.model_weights``).  Returns False when the staging was folded or reused."""
+        if self.cap < self.K or self.staging.generation != self.generation or self.n != self.K:
+            return False  # some updates were overwritten by later chunks, or the slots were reused
+        L, st = self.layout, self.staging
+        kx.reduce(st.x, self.K, L.P, out, denom=float(np.float32(self.K)), finalize=True)
+        acc_i = torch.zeros(L.ldq, dtype=torch.int64, device=self.device)
+        kx.side_accumulate(st.xi, self.K, L.Q, 0, acc_i=acc_i, acc_d=None)
+        kx.side_close(L.Q, 0, float(self.K), acc_i=acc_i, cur=cur_side)
+        return True
 
     # ---- q-FedAvg --------------------------------------------------------------------------------
     def finalize_qfed(self, *, out: torch.Tensor, model_side: torch.Tensor, sqnorm_allreduce=None):

@@ -1,0 +1,84 @@
+"""Edge cases of the device path against the (fixture-pinned) CPU oracle: models with no fp32 entries,
+a single scalar, many clients folded through a small staging buffer, FedBuff and FedYoGi with chunking."""
+import argparse
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.cpu_reference import (OracleAggregator, OracleModel, OracleModelAdapter, OracleServerOptimizer)
+from tests.golden_io import StateDictModule, assert_state_close, assert_state_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _args(policy=None):
+    return argparse.Namespace(gradient_policy=policy, yogi_eta=3e-3, yogi_tau=1e-8, yogi_beta=0.9, yogi_beta2=0.99,
+                              learning_rate=0.05, qfed_q=1.0)
+
+
+def _run(names, init, K, rounds, policy=None, asynchronous=False, capacity=None, seed=0):
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator, DeviceAsyncAggregator
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    args = _args(policy)
+    dev = TorchModelAdapter(StateDictModule(names, init), device="cuda:0", staging_capacity=capacity,
+                            optimizer=TorchServerOptimizer(policy, args, "cuda:0") if policy else None)
+    ref = OracleModelAdapter(OracleModel(names, init), OracleServerOptimizer(policy, args) if policy else None)
+    if asynchronous:
+        agg, oagg = DeviceAsyncAggregator(dev, args), OracleAggregator(ref, args, asynchronous=True)
+        for a in (agg, oagg):
+            a.round = 7
+            a.client_task_model_version = {k: 7 - (k % 5) for k in range(K)}
+    else:
+        agg, oagg = DeviceAggregator(dev, args), OracleAggregator(ref, args)
+    rng = np.random.default_rng(seed)
+    for r in range(rounds):
+        agg.start_round(K)
+        oagg.start_round(K)
+        for k in range(K):
+            upd = []
+            for t in init:
+                if t.dtype == torch.int64:
+                    upd.append(np.array(int(rng.integers(0, 1000)), dtype=np.int64).reshape(tuple(t.shape)))
+                else:
+                    upd.append((t.numpy() + rng.normal(0, 0.01, size=tuple(t.shape))).astype(np.float32))
+            res = {"client_id": k, "update_weight": upd, "moving_loss": float(rng.uniform(0.5, 2))}
+            agg.on_result(res)
+            oagg.on_result(res)
+        yield r, dev.get_weights(), ref.get_weights()
+
+
+def test_int_only_model(gpu_device):
+    names = ["a.num_batches_tracked", "b.num_batches_tracked"]
+    init = [torch.tensor(3), torch.tensor(9)]
+    for r, got, want in _run(names, init, K=5, rounds=2):
+        assert_state_equal(got, [w.numpy() for w in want], f"int-only r{r}")
+
+
+def test_single_scalar_model(gpu_device):
+    for r, got, want in _run(["s"], [torch.tensor(0.25)], K=3, rounds=2):
+        assert_state_equal(got, [w.numpy() for w in want], f"scalar r{r}")
+
+
+@pytest.mark.parametrize("asynchronous", [False, True])
+def test_many_clients_small_staging(gpu_device, asynchronous):
+    names = ["w", "b", "n"]
+    init = [torch.randn(130, 77) * 0.05, torch.randn(77) * 0.05, torch.tensor(4)]
+    for r, got, want in _run(names, init, K=2500, rounds=1, asynchronous=asynchronous, capacity=333):
+        assert_state_equal(got, [w.numpy() for w in want], f"K=2500 cap=333 async={asynchronous}")
+
+
+def test_fedyogi_chunked_three_rounds(gpu_device):
+    names = ["w", "n", "b"]
+    init = [torch.randn(300, 41) * 0.05, torch.tensor(2), torch.randn(41) * 0.05]
+    for r, got, want in _run(names, init, K=37, rounds=3, policy="fed-yogi", capacity=8):
+        assert_state_close(got, [w.numpy() for w in want], 1e-6, f"yogi r{r}")
+
+
+def test_qfedavg_more_clients_than_a_chunk(gpu_device):
+    names = ["w", "n"]
+    init = [torch.randn(2000) * 0.05, torch.tensor(11)]
+    for r, got, want in _run(names, init, K=1300, rounds=1, policy="q-fedavg", capacity=2000):
+        assert_state_close(got, [w.numpy() for w in want], 1e-5, "qfed K=1300", int_slack=1)

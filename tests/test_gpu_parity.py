@@ -87,6 +87,21 @@ def test_model_weights_is_the_fedavg_mean(gpu_device):
             assert np.asarray(g).dtype == np.asarray(w).dtype
 
 
+def test_model_weights_after_qfedavg_round(gpu_device):
+    """The reference keeps the FedAvg mean in model_weights even in q-FedAvg mode (aggregator.py:505-507)."""
+    sc = Scenario("qfedavg_q1")
+    from oracle.cpu_reference import fedavg_close, fedavg_step
+
+    acc = None
+    for k in range(5):
+        acc = fedavg_step(acc, sc.client(k), k == 0)
+    want = fedavg_close(acc, 5)
+    for _, adapter, _, agg in _device_run(sc):
+        got = list(agg.model_weights)
+        for g, w in zip(got, want):
+            np.testing.assert_array_equal(np.asarray(g), np.asarray(w))
+
+
 def test_get_model_syncs_module(gpu_device):
     sc = Scenario("fedavg_femnist_cnn_k10")
     for r, adapter, _, _ in _device_run(sc):
