@@ -19,6 +19,7 @@ import torch
 from ... import _native as N
 
 HB_ELEMS = 1024
+ROW_MODE_MIN = 256  # rows at least this long get one workgroup per (row, 1024 columns)
 
 
 def _dims(shape):
@@ -29,39 +30,76 @@ def _dims(shape):
     return O, I, S
 
 
+class PrefixBoxPlan:
+    """Device-side launch plan for one combination: global tensor dims, per-(client, tensor) box
+    descriptors into the concatenated uploads, and the workgroup -> (tensor, first element) chunk list."""
+
+    def __init__(self, global_shapes: Sequence, local_shapes: Sequence[Sequence], device):
+        self.device = torch.device(device)
+        T, K = len(global_shapes), len(local_shapes)
+        tens = np.zeros((T, 4), dtype=np.int64)
+        goff = 0
+        for k, gs in enumerate(global_shapes):
+            O, I, S = _dims(gs)
+            tens[k] = (goff, O, I, S)
+            goff += O * I * S
+        desc = np.zeros((K, T, 3), dtype=np.int64)
+        off = 0
+        for m, shapes in enumerate(local_shapes):
+            for k, (ls, gs) in enumerate(zip(shapes, global_shapes)):
+                ls, gs = tuple(ls), tuple(gs)
+                O, I, S = _dims(gs)
+                o, i, _ = _dims(ls)
+                if len(ls) != len(gs) or ls[2:] != gs[2:] or o > O or i > I:
+                    raise ValueError(f"client {m} tensor {k}: shape {ls} is not a prefix box of {gs}")
+                desc[m, k] = (off, o, i * S)  # box rows are i*S long in the upload
+                off += o * i * S
+        ck_t, ck_f = [], []  # ck_t holds (tensor, row) pairs; row -1 = element mode
+        for k in range(T):
+            O, RL = int(tens[k, 1]), int(tens[k, 2] * tens[k, 3])
+            if RL >= ROW_MODE_MIN:
+                for o in range(O):
+                    for f in range(0, RL, HB_ELEMS):
+                        ck_t += [k, o]
+                        ck_f.append(f)
+            else:
+                for f in range(0, O * RL, HB_ELEMS):
+                    ck_t += [k, -1]
+                    ck_f.append(f)
+        self.K, self.T, self.P, self.upload_elems = K, T, goff, off
+        self.tens_host = tens
+        self.d_desc = torch.from_numpy(desc.reshape(-1)).to(self.device)
+        self.d_tens = torch.from_numpy(tens.reshape(-1)).to(self.device)
+        self.d_ct = torch.tensor(ck_t, dtype=torch.int32, device=self.device)
+        self.d_cf = torch.tensor(ck_f, dtype=torch.int64, device=self.device)
+        self.nchunks = len(ck_f)
+
+    def run(self, xs: torch.Tensor, glob: torch.Tensor) -> None:
+        """glob (fp32 [P], device) <- HeteroFL combination of the uploads xs (fp32, device, concatenated)."""
+        if xs.numel() < self.upload_elems or glob.numel() < self.P:
+            raise ValueError("PrefixBoxPlan.run: buffers smaller than the plan")
+        for t, n in ((xs, "xs"), (glob, "glob")):
+            if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
+                raise ValueError(f"PrefixBoxPlan.run: {n} must be a contiguous fp32 tensor on {self.device}")
+        N.call("fa_prefix_box_combine", xs.data_ptr(), self.d_desc.data_ptr(), self.K, self.d_tens.data_ptr(),
+               self.T, self.d_ct.data_ptr(), self.d_cf.data_ptr(), self.nchunks, glob.data_ptr(),
+               torch.cuda.current_stream(self.device).cuda_stream)
+
+
 def combine_prefix_boxes(global_state, local_states: Sequence, device=None) -> None:
     """In place: global_state (an ordered name -> tensor mapping, e.g. ``model.state_dict()``) takes the
     HeteroFL combination of ``local_states`` (per client: mapping name -> prefix-box tensor/array)."""
     dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
     names = list(global_state.keys())
-    T, K = len(names), len(local_states)
-    if K == 0:
+    if not local_states:
         return
-    tens = np.zeros((T, 4), dtype=np.int64)
-    goff = 0
-    for k, n in enumerate(names):
-        v = global_state[n]
-        if v.dtype != torch.float32:
-            raise NotImplementedError(f"{n}: HeteroFL combination supports float32 entries (got {v.dtype})")
-        O, I, S = _dims(v.shape)
-        tens[k] = (goff, O, I, S)
-        goff += O * I * S
-    desc = np.zeros((K, T, 3), dtype=np.int64)
-    sizes = []
-    off = 0
-    for m, loc in enumerate(local_states):
-        for k, n in enumerate(names):
-            a = loc[n]
-            shp = tuple(a.shape)
-            gshape = tuple(global_state[n].shape)
-            O, I, S = _dims(gshape)
-            o, i, s = _dims(shp)
-            if len(shp) != len(gshape) or shp[2:] != gshape[2:] or o > O or i > I:
-                raise ValueError(f"client {m} {n}: shape {shp} is not a prefix box of {gshape}")
-            desc[m, k] = (off, o, i)
-            off += o * i * S
-            sizes.append(o * i * S)
-    xs_host = torch.empty(max(off, 1), dtype=torch.float32, pin_memory=True)
+    for n in names:
+        if global_state[n].dtype != torch.float32:
+            raise NotImplementedError(f"{n}: HeteroFL combination supports float32 entries "
+                                      f"(got {global_state[n].dtype})")
+    plan = PrefixBoxPlan([tuple(global_state[n].shape) for n in names],
+                         [[tuple(loc[n].shape) for n in names] for loc in local_states], dev)
+    xs_host = torch.empty(max(plan.upload_elems, 1), dtype=torch.float32, pin_memory=True)
     xv = xs_host.numpy()
     pos = 0
     for loc in local_states:
@@ -72,25 +110,12 @@ def combine_prefix_boxes(global_state, local_states: Sequence, device=None) -> N
                 raise TypeError(f"{n}: local dtype {a.dtype}, expected float32")
             xv[pos:pos + a.size] = a.reshape(-1)
             pos += a.size
-    glob_host = torch.cat([global_state[n].detach().reshape(-1).cpu() for n in names]) if T else torch.zeros(0)
-    ck_t, ck_f = [], []
-    for k in range(T):
-        n_el = int(tens[k, 1] * tens[k, 2] * tens[k, 3])
-        for f in range(0, n_el, HB_ELEMS):
-            ck_t.append(k)
-            ck_f.append(f)
-    xs = xs_host.to(dev, non_blocking=True)
-    glob = glob_host.to(dev)
-    d_desc = torch.from_numpy(desc.reshape(-1)).to(dev)
-    d_tens = torch.from_numpy(tens.reshape(-1)).to(dev)
-    d_ct = torch.tensor(ck_t, dtype=torch.int32, device=dev)
-    d_cf = torch.tensor(ck_f, dtype=torch.int64, device=dev)
-    N.call("fa_prefix_box_combine", xs.data_ptr(), d_desc.data_ptr(), K, d_tens.data_ptr(), T, d_ct.data_ptr(),
-           d_cf.data_ptr(), len(ck_t), glob.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+    glob = torch.cat([global_state[n].detach().reshape(-1).cpu() for n in names]).to(dev)
+    plan.run(xs_host.to(dev, non_blocking=True), glob)
     out = glob.cpu()
     for k, n in enumerate(names):
         v = global_state[n]
-        v.copy_(out[int(tens[k, 0]):int(tens[k, 0]) + v.numel()].view(v.shape))
+        v.copy_(out[int(plan.tens_host[k, 0]):int(plan.tens_host[k, 0]) + v.numel()].view(v.shape))
 
 
 class DeviceHeteroFLMixin:

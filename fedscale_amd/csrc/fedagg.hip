@@ -815,29 +815,65 @@ extern "C" int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uin
 // a workgroup covers HB_ELEMS elements of ONE tensor, so the per-client box descriptors are uniform
 // (scalar loads) and a client's covered elements are contiguous runs of its upload.
 #define HB_ELEMS 1024
+#ifndef HB_U
+#define HB_U 8
+#endif  // HB_U: clients whose loads are issued before their (in-order) adds
 
+// desc[(m*T + k)*3 + {0,1,2}] = {offset of client m's box of tensor k in xs, o_m, L_m = i_m*S}
+// (host-precomputed row length).  A chunk is (tensor k, row o >= 0, first column r0) in ROW mode, where
+// o is uniform so "client m covers this row" is a scalar branch and the covered columns are the prefix
+// r < L_m of the row; or (k, -1, first element) in ELEMENT mode for tensors with short rows (1-D ...).
 __global__ __launch_bounds__(256) void k_prefix_box(const float* __restrict__ xs, const int64_t* __restrict__ desc,
                                                     int K, int T, const int64_t* __restrict__ tens,
                                                     const int32_t* __restrict__ ck_t,
                                                     const int64_t* __restrict__ ck_first, float* glob) {
   const int c = blockIdx.x;
-  const int k = ck_t[c];
-  const int64_t goff = tens[4 * k], I = tens[4 * k + 2], S = tens[4 * k + 3];
-  const int64_t n = tens[4 * k + 1] * I * S;
+  const int k = ck_t[2 * c];
+  const int row = ck_t[2 * c + 1];
+  const int64_t goff = tens[4 * k];
+  const int64_t RL = tens[4 * k + 2] * tens[4 * k + 3];  // global row length I*S
+  const int64_t n = tens[4 * k + 1] * RL;
+  const int64_t* dk = desc + 3 * (int64_t)k;
+  const int64_t dstride = 3 * (int64_t)T;
   for (int j = 0; j < HB_ELEMS / 256; ++j) {
-    const int64_t e = ck_first[c] + j * 256 + threadIdx.x;
-    if (e >= n) break;
-    const int64_t o = e / (I * S), r = e - o * I * S, i = r / S, s = r - i * S;
+    int64_t o, r;
+    if (row >= 0) {
+      o = row;
+      r = ck_first[c] + j * 256 + threadIdx.x;
+      if (r >= RL) break;
+    } else {
+      const int64_t e = ck_first[c] + j * 256 + threadIdx.x;
+      if (e >= n) break;
+      o = e / RL;
+      r = e - o * RL;
+    }
     float acc = 0.f;  // tmp_v = v.new_zeros(..., dtype=torch.float32)
     int cnt = 0;
-    for (int m = 0; m < K; ++m) {
-      const int64_t* d = desc + 3 * ((int64_t)m * T + k);
-      if (o < d[1] && i < d[2]) {
-        acc = acc + xs[d[0] + (o * d[2] + i) * S + s];  // tmp_v[idx] += local_parameters[k]
-        ++cnt;                                          // count[k][idx] += 1
+    int m = 0;
+    for (; m + HB_U <= K; m += HB_U) {
+      float t[HB_U];
+      bool hit[HB_U];
+#pragma unroll
+      for (int u = 0; u < HB_U; ++u) {
+        const int64_t* d = dk + (int64_t)(m + u) * dstride;
+        hit[u] = o < d[1] && r < d[2];
+        t[u] = hit[u] ? xs[d[0] + o * d[2] + r] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < HB_U; ++u)
+        if (hit[u]) {
+          acc = acc + t[u];  // tmp_v[idx] += local_parameters[k], clients in order
+          ++cnt;             // count[k][idx] += 1
+        }
+    }
+    for (; m < K; ++m) {
+      const int64_t* d = dk + (int64_t)m * dstride;
+      if (o < d[1] && r < d[2]) {
+        acc = acc + xs[d[0] + o * d[2] + r];
+        ++cnt;
       }
     }
-    if (cnt > 0) glob[goff + e] = __fdiv_rn(acc, (float)cnt);  // tmp_v[count>0].div_(count[count>0])
+    if (cnt > 0) glob[goff + o * RL + r] = __fdiv_rn(acc, (float)cnt);  // tmp_v[count>0].div_(count[..])
   }
 }
 

@@ -150,9 +150,10 @@ int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uint32_t seed,
  * HeteroFL sub-model combination: replaces Customized_Aggregator.combine_models,
  * examples/heterofl/customized_aggregator.py:78-119 (index sets from customized_fllibs.py:25-70 are
  * prefixes, so client m's upload of tensor k is the box [0:o) x [0:i) x S of the global (O, I, S)).
- *   xs       concatenated client uploads (fp32), desc[(m*T + k)*3 + {0,1,2}] = {offset in xs, o, i}
- *   tensors  [T][4] = {offset in global, O, I, S};  chunks: workgroup c covers elements
- *            [chunk_first[c], chunk_first[c] + 1024) of tensor chunk_tensor[c]
+ *   xs       concatenated client uploads (fp32), desc[(m*T + k)*3 + {0,1,2}] = {offset in xs, o, i*S}
+ *   tensors  [T][4] = {offset in global, O, I, S};  chunk_tensor[2c] = tensor of workgroup c,
+ *            chunk_tensor[2c+1] = row o (>= 0: columns [chunk_first[c], +1024) of that row) or -1
+ *            (elements [chunk_first[c], +1024) of the flattened tensor)
  * global[e] <- (sum over covering clients, client order, fp32 from 0) / fp32(count) where count > 0.
  */
 int fa_prefix_box_combine(const float* xs, const int64_t* desc, int32_t K, const int64_t* tensors, int32_t T,

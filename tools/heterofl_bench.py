@@ -1,0 +1,60 @@
+"""Device-resident HeteroFL combination rate (examples/heterofl/customized_aggregator.py:78-119) on a
+ResNet-18 layout: K clients at model rates drawn like the example's config (80 % rate 1, 20 % rate 0.5).
+usage: python tools/heterofl_bench.py [K] [reps]"""
+import json
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    K = int(sys.argv[1]) if len(sys.argv) > 1 else 100
+    reps = int(sys.argv[2]) if len(sys.argv) > 2 else 10
+    from fedscale_amd import synth
+    from fedscale_amd.cloud.aggregation.heterofl import PrefixBoxPlan
+
+    names, shapes, dtypes = synth.resnet18_layout()
+    gshapes = [s for s, d in zip(shapes, dtypes) if d == torch.float32]
+    rates = [1.0 if m % 5 else 0.5 for m in range(K)]
+
+    def box(s, r, first):
+        if len(s) >= 2:  # conv / linear weight: output and input prefixes (first conv keeps its 3 inputs)
+            o = s[0] if s[0] == 10 else math.ceil(r * s[0])
+            i = s[1] if first else math.ceil(r * s[1])
+            return (o, i) + tuple(s[2:])
+        if len(s) == 1:
+            return (s[0],) if s[0] == 10 else (math.ceil(r * s[0]),)
+        return s
+
+    lshapes = [[box(s, r, k == 0) for k, s in enumerate(gshapes)] for r in rates]
+    plan = PrefixBoxPlan(gshapes, lshapes, "cuda:0")
+    xs = torch.empty(1, plan.upload_elems, device="cuda:0")
+    synth.fill(xs, 1, plan.upload_elems, seed=9)
+    xs = xs[0]
+    glob = torch.empty(1, plan.P + 64, device="cuda:0")
+    synth.fill(glob, 1, plan.P, seed=10)
+    glob = glob[0]
+    plan.run(xs, glob)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        plan.run(xs, glob)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    alg = 4 * plan.upload_elems + 8 * plan.P  # every upload element read once; global read + written
+    out = {"K": K, "P": plan.P, "upload_elems": plan.upload_elems, "kernel_ms": ms,
+           "GBps": alg / (ms * 1e-3) / 1e9, "client_updates_per_s": K / (ms * 1e-3)}
+    print(json.dumps(out))
+    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "heterofl_bench.json"), "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
