@@ -1,0 +1,41 @@
+"""Property tests (hypothesis) of the bucket layout: for any state_dict shape list and any world size,
+the shards tile the fp32 vector exactly, are equal-size and 64-aligned, and pack -> gather -> unpack is
+the identity (the host half of the sharded path; CPU only)."""
+import numpy as np
+import torch
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from fedscale_amd.bucket import ALIGN, BucketLayout
+
+shape = st.lists(st.integers(0, 9), min_size=0, max_size=3).map(tuple)
+entry = st.tuples(shape, st.sampled_from([torch.float32, torch.float32, torch.int64]))
+
+
+@settings(max_examples=60, deadline=None)
+@given(st.lists(entry, min_size=1, max_size=8), st.integers(1, 9), st.integers(0, 2**31 - 1))
+def test_shards_tile_and_roundtrip(entries, world, seed):
+    names = [f"e{i}" for i in range(len(entries))]
+    shapes = [e[0] for e in entries]
+    dtypes = [e[1] for e in entries]
+    full = BucketLayout(names, shapes, dtypes)
+    rng = np.random.default_rng(seed)
+    vals = [rng.normal(size=s).astype(np.float32) if d == torch.float32
+            else np.asarray(rng.integers(-5, 5, size=s), dtype=np.int64) for s, d in zip(shapes, dtypes)]
+    parts = []
+    side = None
+    ld0 = BucketLayout(names, shapes, dtypes, 0, world).ld
+    for r in range(world):
+        lay = BucketLayout(names, shapes, dtypes, r, world)
+        assert lay.ld == ld0 and lay.ld % ALIGN == 0 and lay.P <= lay.ld
+        f = np.zeros(lay.ld, np.float32)
+        i = np.zeros(lay.ldq, np.int64)
+        lay.pack_host(vals, f, i, workers=2)
+        parts.append(f)
+        side = i if side is None else side
+        np.testing.assert_array_equal(side, i)  # the side table is replicated
+    assert sum(BucketLayout(names, shapes, dtypes, r, world).P for r in range(world)) == full.P_full
+    flat = np.concatenate(parts)
+    out = full.unpack(torch.from_numpy(flat), torch.from_numpy(side))
+    for o, v in zip(out, vals):
+        np.testing.assert_array_equal(o.numpy(), v)
