@@ -19,6 +19,8 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <unistd.h>
+
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -278,7 +280,10 @@ static void launch_plan(const RedArgs& r, hipStream_t st) {
 #if FA_LEVELS == 1
   launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, false, st);
 #else
-  col = launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, true, st);
+#ifndef FA_YOGI_SKIP_L0
+#define FA_YOGI_SKIP_L0 0
+#endif
+  if (!(EPI == EPI_YOGI && FA_YOGI_SKIP_L0)) col = launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, true, st);
   if (col < r.P4) col = launch_level<FA_L1_V, FA_L1_U, EPI, W>(r, col, r.P4, true, st);
   if (col < r.P4) col = launch_level<FA_L2_V, FA_L2_U, EPI, W>(r, col, r.P4, true, st);
   if (col < r.P4) launch_level<FA_L3_V, FA_L3_U, EPI, W>(r, col, r.P4, false, st);
@@ -942,6 +947,7 @@ struct GatherPool {
 };
 std::mutex g_pool_mu;
 GatherPool* g_pool = nullptr;
+pid_t g_pool_pid = 0;  // a forked child inherits the pointer but not the threads: rebuild there
 }  // namespace
 
 extern "C" int fa_host_gather(void* dst, const void* const* srcs, const int64_t* dst_off, const int64_t* nbytes,
@@ -959,9 +965,17 @@ extern "C" int fa_host_gather(void* dst, const void* const* srcs, const int64_t*
   }
   if (threads > 64) threads = 64;
   std::lock_guard<std::mutex> serial(g_pool_mu);  // one gather at a time through the shared pool
-  if (!g_pool || g_pool->nthreads != threads) {
-    delete g_pool;
-    g_pool = new GatherPool(threads);
+  try {
+    if (g_pool && g_pool_pid != getpid()) g_pool = nullptr;  // inherited across fork(): leak, do not join
+    if (!g_pool || g_pool->nthreads != threads) {
+      delete g_pool;
+      g_pool = new GatherPool(threads);
+      g_pool_pid = getpid();
+    }
+  } catch (...) {  // no exception crosses the C ABI: fall back to one thread
+    g_pool = nullptr;
+    for (int i = 0; i < n; ++i) memcpy(d + dst_off[i], srcs[i], (size_t)nbytes[i]);
+    return FA_OK;
   }
   const int64_t share = (total + threads - 1) / threads;
   g_pool->run([&](int w) {
