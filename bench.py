@@ -44,6 +44,8 @@ def parse():
     ap.add_argument("--reassemble", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample (0 = skip)")
     ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--no-other-configs", action="store_true",
+                    help="skip the BASELINE configs 2/3 side measurements (reported under other_configs)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse ranks sharing a GPU")
     return ap.parse_args()
@@ -78,6 +80,45 @@ def cpu_baseline(K: int, P: int, budget_s: float, seed: int) -> dict:
                       f"(pool of {pool_n} distinct 100 MB buffers), {t_acc * 1e3:.1f} ms/client + "
                       f"{t_fin * 1e3:.0f} ms finalize, extrapolated linearly to K={K}",
             "host": platform.processor() or platform.machine(), "host_cpus": os.cpu_count()}
+
+
+def other_configs(dev, seed: int) -> dict:
+    """BASELINE.json configs 2 and 3 on one GPU (FedAvg, device-resident), beside the headline line.
+    Config 2 (400 MB) rotates two input sets so the 256 MiB Infinity Cache cannot serve repeats."""
+    import numpy as np
+    import torch
+
+    from fedscale_amd import kernels as kx
+    from fedscale_amd import synth
+    from fedscale_amd.bucket import round_up
+
+    out = {}
+    for name, K, P, sets in (("c2_synthetic_k100_p1M", 100, 1_000_000, 2),
+                             ("c3_resnet18_layout_k1000_p11191242", 1000, 11_191_242, 1)):
+        ld = round_up(P, 64)
+        xs = []
+        for i in range(sets):
+            x = torch.empty(K, ld, dtype=torch.float32, device=dev)
+            synth.fill(x, K, P, seed=seed + 31 * i)
+            xs.append(x)
+        o = torch.empty(ld, dtype=torch.float32, device=dev)
+        for i in range(4):
+            kx.reduce(xs[i % sets], K, P, o, denom=float(np.float32(K)), finalize=True)
+        torch.cuda.synchronize(dev)
+        evs = []
+        for i in range(20):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            kx.reduce(xs[i % sets], K, P, o, denom=float(np.float32(K)), finalize=True)
+            e1.record()
+            evs.append((e0, e1))
+        torch.cuda.synchronize(dev)
+        ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
+        out[name] = {"clients": K, "params": P, "kernel_ms": ms, "client_updates_per_s": K / (ms * 1e-3),
+                     "hbm_gbps": (4 * K * P + 4 * P) / (ms * 1e-3) / 1e9}
+        del xs, o
+        torch.cuda.empty_cache()
+    return out
 
 
 def main():
@@ -234,8 +275,12 @@ def main():
         }
         if reassembly_ms is not None:
             res["reassembly_ms"] = reassembly_ms
-        if world == 1 and args.cpu_seconds > 0:
+        if world == 1 and not args.no_other_configs:
             del x
+            torch.cuda.empty_cache()
+            res["other_configs"] = other_configs(dev, args.seed)
+        if world == 1 and args.cpu_seconds > 0:
+            x = None
             torch.cuda.empty_cache()
             res["cpu_baseline"] = cpu_baseline(K, P, args.cpu_seconds, args.seed)
         else:
