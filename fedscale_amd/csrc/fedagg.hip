@@ -385,25 +385,32 @@ extern "C" int fa_yogi_step(const float* cur, const float* last, float* m, float
 // ------------------------------------------------------------------------------------------------
 // q-FedAvg phase 1: delta chain + per-client sum of squares
 // ------------------------------------------------------------------------------------------------
-// Layout: a fixed grid of QF_GRID workgroups (4 waves each) grid-strides over column tiles of QF_V KiB
-// per wave; the grid size is a constant so the fp64 sum-of-squares order is deterministic across runs
-// and devices.  Clients are taken in groups of 8: per client each lane sums its QF_V*4 squares in fp64
-// (v[j]); after the group, one "multi-reduce" butterfly (xor 32 / 16 / 8 halve the value set, xor 4 /
-// 2 / 1 finish) leaves lane l with the wave total of client (l >> 3) & 7 — 10 fp64 shuffles per 8
-// clients instead of 48 — and lanes l % 8 == 0 add it into the LDS slot [wave][k].  At the end the
+// Layout: a fixed grid of QF_GRID workgroups (4 waves each), each owning an equal contiguous run of
+// columns that it walks in tiles of QF_V KiB per wave; the grid size is a constant so the fp64
+// sum-of-squares order is deterministic across runs and devices.  Clients are taken in groups of QF_G
+// (8 or 4): per client each lane sums its QF_V*4 squares in fp64 (v[j]); after the group, one
+// "multi-reduce" butterfly (for 8: xor 32 / 16 / 8 halve the value set, xor 4 / 2 / 1 finish) leaves
+// lane l with the wave total of client (l >> 3) & 7 — 10 fp64 shuffles per 8 clients instead of 48 —
+// and the first lane of each client's lane group adds it into the LDS slot [wave][k].  At the end the
 // block writes its 4-wave total per client to workspace[block][k]; k_qfed_gather sums the blocks in
 // block order.  No atomics: bit-reproducible run to run.
 #ifndef QF_V
-#define QF_V 8
+#define QF_V 16
 #endif
 #ifndef QF_U
 #define QF_U 1
 #endif
-#define QF_G 8
+#ifndef QF_G
+#define QF_G 4  // clients per multi-reduce group: 4 or 8
+#endif
+static_assert(QF_G == 8 || QF_G == 4, "QF_G must be 4 or 8");
 #ifndef QF_GRID
-#define QF_GRID 512  // = 2 workgroups x 256 CUs resident at 2 waves/SIMD (profiles/r01_tune_qfed.log)
+#define QF_GRID 256  // one workgroup per CU at 1 wave/SIMD (profiles/r01_tune_qfed.log)
 #endif
 
+#ifndef QF_BALANCE
+#define QF_BALANCE 1  // 0: always full-width tiles (plain grid-stride)
+#endif
 #define QF_MAXK 1024  // LDS: 4 waves x 1024 clients x 8 B = 32 KiB per workgroup
 
 struct QfArgs {
@@ -415,6 +422,7 @@ struct QfArgs {
   const float* alpha;
   float lr, rlr;  // rlr = RN(1/lr)
   int fast;       // 0: lr outside [2^-20, 2^20] -> IEEE division for every element
+  int sw;         // strips (64 f4 columns) per wave per tile, <= QF_V
   float* delta;
   double* part;  // [gridDim.x][K]
 };
@@ -422,24 +430,52 @@ struct QfArgs {
 // a / b for a runtime-constant divisor b with r = RN(1/b): q = RN(a*r), then one exact-residual
 // correction q + (a - b*q)*r.  Markstein's theorem: r correctly rounded and q within 1 ulp make the
 // corrected quotient the correctly rounded a/b (a quotient has no midpoint cases).  It needs a normal
-// residual and quotient: the host admits only 2^-20 <= |b| <= 2^20 for this path, and per element
-// |a| in [2^-80, 2^80] or a == 0 (fast_div_ok); any other element (denormal, huge, inf, NaN) makes its
-// wave redo that client with the IEEE division (rare, checked once per client with a wave vote).
+// residual and quotient: the host admits only 2^-20 <= |b| <= 2^20 for this path, and every element of
+// the client must have |a| in [2^-80, 2^80) or a == 0 (NaN propagates correctly either way); otherwise
+// (a denormal, huge or infinite element anywhere in the wave) the wave redoes that client with the
+// IEEE division.  The range test is folded per lane into min/max of frexp exponents + max |a|, one wave
+// vote per client.
 __device__ __forceinline__ float fast_div(float a, float b, float r) {
   const float q = a * r;
   const float rem = __builtin_fmaf(-q, b, a);
   return __builtin_fmaf(rem, r, q);
 }
-__device__ __forceinline__ bool fast_div_ok(float a) {
-  const uint32_t m = __builtin_bit_cast(uint32_t, a) & 0x7fffffffu;
-  return (m - 0x17800000u) < (0x67800000u - 0x17800000u) || m == 0u;  // [2^-80, 2^80) or +-0
-}
+struct DivRange {
+  int emin = 0, emax = 0;  // frexp exponents (0 for +-0): |a| in [2^(e-1), 2^e)
+  float amax = 0.f;        // catches +-inf (frexp reports 0 for it)
+  __device__ __forceinline__ void add(float a) {
+    const int e = __builtin_amdgcn_frexp_expf(a);
+    emin = e < emin ? e : emin;
+    emax = e > emax ? e : emax;
+    amax = __builtin_fmaxf(amax, __builtin_fabsf(a));
+  }
+  __device__ __forceinline__ bool ok() const { return emin >= -79 && emax <= 80 && amax < __builtin_inff(); }
+};
 
 __device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xor(v, m, 64); }
 
+// Client rows are read through buffer descriptors (cdna guide T8) and every mask is an offset: a lane
+// whose column is past P (or past its wave's sw strips) gets the voffset sentinel QF_OOB, which is past
+// num_records, so the hardware returns zero without touching memory — one load path, no exec masking.
+//  * WIDE (QF_G rows span < 2 GiB): ONE descriptor per client group, base = the group's first row,
+//    num_records = its valid rows only; voffset = column + row * rowbytes, so rows of clients past K are
+//    out of range too.
+//  * otherwise: one descriptor per client row, num_records = the row's P4 * 16 bytes (rows past K: 0);
+//    the host cuts P into column windows of < 2 GiB (fa_qfed_accumulate).
+// aux 2 = non-temporal.
+#define QF_OOB 0x80000000u
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* row0, uint32_t nbytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(row0), (short)0, (int)nbytes, 0x00020000);
+}
+__device__ __forceinline__ f4 rows_load(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 2));
+}
+
 #ifndef QF_MINW
-#define QF_MINW 2
+#define QF_MINW 1
 #endif
+// WIDE: one descriptor spans all QF_G rows of a group (QF_G rows < 4 GiB); otherwise one per QF_U rows.
+template <bool WIDE>
 __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
   __shared__ double sq[4][QF_MAXK];
   const int lane = threadIdx.x & 63;
@@ -447,22 +483,32 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
   for (int i = threadIdx.x; i < 4 * QF_MAXK; i += 256) (&sq[0][0])[i] = 0.0;
   __syncthreads();
 
-  const f4* __restrict__ xp = reinterpret_cast<const f4*>(q.x);
-  const int64_t tile_cols = 4LL * 64 * QF_V;
-  const int64_t ntiles = (q.P4 + tile_cols - 1) / tile_cols;
+  // Balanced grid-stride: the columns come in strips of 64 f4 (one wave-wide dwordx4 load).  A tile is
+  // 4 waves x sw strips, sw <= QF_V chosen so that the tiles divide evenly over the grid (fa_qfed_
+  // accumulate: q.sw) — no workgroup is left with an extra tile whatever P is — and the workgroups
+  // stride over tiles so the grid's concurrent loads stay on adjacent addresses.
+  const int64_t S = (q.P4 + 63) / 64;
+  const int sw = q.sw;
+  const int64_t ntiles = (S + 4 * sw - 1) / (4 * sw);
+  const uint32_t rowbytes = (uint32_t)(q.ld4 * 16);
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const int64_t c0 = tile * tile_cols + (int64_t)wave * 64 * QF_V + lane;
+    const int64_t sw0 = tile * 4 * sw + (int64_t)wave * sw;  // this wave's first strip
+    const int64_t c0 = sw0 * 64 + lane;
     bool ok[QF_V];
     f4 L[QF_V], D[QF_V];
+    uint32_t voff[QF_V];  // byte offset of this lane's column j in a row, or QF_OOB
 #pragma unroll
     for (int j = 0; j < QF_V; ++j) {
-      ok[j] = (c0 + 64 * j) < q.P4;
+      ok[j] = j < sw && (c0 + 64 * j) < q.P4;
+      voff[j] = ok[j] ? (uint32_t)((c0 + 64 * j) * 16) : QF_OOB;
       L[j] = ok[j] ? reinterpret_cast<const f4*>(q.last)[c0 + 64 * j] : f4{0.f, 0.f, 0.f, 0.f};
       D[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.delta)[c0 + 64 * j]
                                                   : f4{0.f, 0.f, 0.f, 0.f};
     }
-    const f4* row = xp + c0;
     for (int kg = 0; kg < q.K; kg += QF_G) {
+      const int nrows = q.K - kg < QF_G ? q.K - kg : QF_G;
+      const float* row0 = q.x + (int64_t)kg * q.ld4 * 4;
+      const __amdgpu_buffer_rsrc_t grp = rows_rsrc(row0, WIDE ? (uint32_t)nrows * rowbytes : 0u);
       double v[QF_G];
 #pragma unroll
       for (int jj = 0; jj < QF_G; ++jj) v[jj] = 0.0;
@@ -470,11 +516,17 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       for (int u0 = 0; u0 < QF_G; u0 += QF_U) {
         f4 t[QF_U][QF_V];
 #pragma unroll
-        for (int u = 0; u < QF_U; ++u)
+        for (int u = 0; u < QF_U; ++u) {
+          if (WIDE) {
 #pragma unroll
-          for (int j = 0; j < QF_V; ++j)
-            t[u][j] = (ok[j] && kg + u0 + u < q.K) ? ldnt(row + (int64_t)(u0 + u) * q.ld4 + 64 * j)
-                                                   : f4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < QF_V; ++j) t[u][j] = rows_load(grp, voff[j] + (uint32_t)(u0 + u) * rowbytes);
+          } else {
+            const __amdgpu_buffer_rsrc_t rr =
+                rows_rsrc(row0 + (int64_t)(u0 + u) * q.ld4 * 4, u0 + u < nrows ? (uint32_t)(q.P4 * 16) : 0u);
+#pragma unroll
+            for (int j = 0; j < QF_V; ++j) t[u][j] = rows_load(rr, voff[j]);
+          }
+        }
 #pragma unroll
         for (int u = 0; u < QF_U; ++u) {
           const int kk = kg + u0 + u;
@@ -482,7 +534,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
           const float al = q.alpha[kk];
           const bool first = (kk == 0) && !(q.flags & FA_ACCUMULATE);
           f4 g[QF_V];
-          bool good = true;
+          DivRange rng;
 #pragma unroll
           for (int j = 0; j < QF_V; ++j) {
             t[u][j] = L[j] - t[u][j];  // (last - W), optimizers.py:83; the "* 1.0" is exact
@@ -490,10 +542,12 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
             g[j].y = fast_div(t[u][j].y, q.lr, q.rlr);
             g[j].z = fast_div(t[u][j].z, q.lr, q.rlr);
             g[j].w = fast_div(t[u][j].w, q.lr, q.rlr);
-            good = good && fast_div_ok(t[u][j].x) && fast_div_ok(t[u][j].y) && fast_div_ok(t[u][j].z) &&
-                   fast_div_ok(t[u][j].w);
+            rng.add(t[u][j].x);
+            rng.add(t[u][j].y);
+            rng.add(t[u][j].z);
+            rng.add(t[u][j].w);
           }
-          if (!q.fast || !__all(good)) {  // rare: redo this client with the IEEE division
+          if (!q.fast || !__all(rng.ok())) {  // rare: redo this client with the IEEE division
 #pragma unroll
             for (int j = 0; j < QF_V; ++j) {
               g[j].x = __fdiv_rn(t[u][j].x, q.lr);
@@ -513,10 +567,11 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
           v[u0 + u] = acc;
         }
       }
-      row += QF_G * q.ld4;
-      // multi-reduce: 8 values per lane -> lane l holds the wave sum of client (l >> 3) & 7
-      double w4[4], w2[2], y;
+      // multi-reduce: QF_G values per lane -> lane l holds the wave sum of client (l >> s) & (QF_G-1)
+      double y;
       const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
+#if QF_G == 8
+      double w4[4], w2[2];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const double keep = b5 ? v[i + 4] : v[i], send = b5 ? v[i] : v[i + 4];
@@ -531,11 +586,27 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
         const double keep = b3 ? w2[1] : w2[0], send = b3 ? w2[0] : w2[1];
         y = keep + shfl_xor_d(send, 8);
       }
+      constexpr int csh = 3;  // client index bits: lane bits 5..3
+#else
+      double w2[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const double keep = b5 ? v[i + 2] : v[i], send = b5 ? v[i] : v[i + 2];
+        w2[i] = keep + shfl_xor_d(send, 32);
+      }
+      {
+        const double keep = b4 ? w2[1] : w2[0], send = b4 ? w2[0] : w2[1];
+        y = keep + shfl_xor_d(send, 16);
+      }
+      y += shfl_xor_d(y, 8);
+      (void)b3;
+      constexpr int csh = 4;  // client index bits: lane bits 5..4
+#endif
       y += shfl_xor_d(y, 4);
       y += shfl_xor_d(y, 2);
       y += shfl_xor_d(y, 1);
-      const int jcl = (lane >> 3) & 7;
-      if ((lane & 7) == 0 && kg + jcl < q.K) sq[wave][kg + jcl] += y;
+      const int jcl = (lane >> csh) & (QF_G - 1);
+      if ((lane & ((1 << csh) - 1)) == 0 && kg + jcl < q.K) sq[wave][kg + jcl] += y;
     }
 #pragma unroll
     for (int j = 0; j < QF_V; ++j)
@@ -569,17 +640,39 @@ extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t
     return fail(FA_E_ARG, "fa_qfed_accumulate: x/last/delta must be 16-byte aligned");
   QfArgs q{};
   if (!(lr > 1e-30f && lr < 1e30f)) return fail(FA_E_ARG, "fa_qfed_accumulate: lr=%g outside (1e-30, 1e30)", (double)lr);
-
   q.x = x; q.ld4 = ld / 4; q.P4 = (P + 3) / 4; q.K = K; q.flags = flags; q.last = last; q.alpha = alpha;
   q.lr = lr; q.rlr = 1.0f / lr; q.delta = delta; q.part = (double*)workspace;
   q.fast = (lr >= 9.5367432e-07f && lr <= 1048576.f) ? 1 : 0;  // [2^-20, 2^20]
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_qfed_accum, dim3(QF_GRID), dim3(256), 0, st, q);
-  int e = check_launch("fa_qfed_accumulate");
-  if (e) return e;
-  hipLaunchKernelGGL(k_qfed_gather, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)workspace,
-                     (int)QF_GRID, (int)K, sqnorm);
-  return check_launch("fa_qfed_accumulate(gather)");
+  // WIDE needs QF_G rows plus the sentinel below 2^32; otherwise per-row descriptors over column
+  // windows of 2^28 floats (1 GiB), one launch each; the gathers add their partial norms in order.
+  const bool wide = (int64_t)ld * 4 * QF_G <= (1LL << 31);
+  const int64_t win = wide ? (P > 0 ? P : 1) : (1LL << 28);
+  for (int64_t w0 = 0; w0 < P || w0 == 0; w0 += win) {
+    QfArgs qw = q;
+    const int64_t pw = P - w0 < win ? P - w0 : win;
+    qw.x = x + w0; qw.last = last + w0; qw.delta = delta + w0; qw.P4 = (pw + 3) / 4;
+    {  // rounds r = tiles per workgroup at full width; then the narrowest tile that still needs r rounds
+      const int64_t S = (qw.P4 + 63) / 64;
+      const int64_t r = (S + (int64_t)QF_GRID * 4 * QF_V - 1) / ((int64_t)QF_GRID * 4 * QF_V);
+      const int64_t strips = r > 0 ? (S + (int64_t)QF_GRID * r - 1) / ((int64_t)QF_GRID * r) : 1;
+      qw.sw = (int)((strips + 3) / 4);
+      if (qw.sw < 1) qw.sw = 1;
+      if (qw.sw > QF_V || !QF_BALANCE) qw.sw = QF_V;
+    }
+    if (wide)
+      hipLaunchKernelGGL(k_qfed_accum<true>, dim3(QF_GRID), dim3(256), 0, st, qw);
+    else
+      hipLaunchKernelGGL(k_qfed_accum<false>, dim3(QF_GRID), dim3(256), 0, st, qw);
+    int e = check_launch("fa_qfed_accumulate");
+    if (e) return e;
+    hipLaunchKernelGGL(k_qfed_gather, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)workspace,
+                       (int)QF_GRID, (int)K, sqnorm);
+    e = check_launch("fa_qfed_accumulate(gather)");
+    if (e) return e;
+    if (pw >= P - w0) break;
+  }
+  return FA_OK;
 }
 
 __global__ void k_qfed_hs(const double* sqnorm, const float* c1, const float* c2, int K, float* hs_out) {

@@ -82,3 +82,38 @@ def test_qfedavg_more_clients_than_a_chunk(gpu_device):
     init = [torch.randn(2000) * 0.05, torch.tensor(11)]
     for r, got, want in _run(names, init, K=1300, rounds=1, policy="q-fedavg", capacity=2000):
         assert_state_close(got, [w.numpy() for w in want], 1e-5, "qfed K=1300", int_slack=1)
+
+
+@pytest.mark.parametrize("K,P", [(3, (1 << 28) + 1000), (5, 140_000_003)])
+def test_qfed_accumulate_wide_rows_and_column_windows(gpu_device, K, P):
+    """Rows longer than the one-descriptor-per-group limit (4 rows x 4 B x ld > 2 GiB) take the
+    per-row-descriptor path, and P > 2^28 is cut into column windows; a ragged K exercises rows past K.
+    delta is bit-exact against torch fp32 on the same device (IEEE division, same per-element order);
+    the squared norms to 1e-9 (fp32 4-square partials summed in fp64, as the kernel documents)."""
+    from fedscale_amd import kernels as kx
+    from fedscale_amd import synth
+    from fedscale_amd.bucket import round_up
+
+    ld = round_up(P, 64)
+    x = torch.empty(K, ld, device="cuda")
+    synth.fill(x, K, P, seed=11)
+    last = torch.empty(1, ld, device="cuda")
+    synth.fill(last, 1, P, seed=11 + 90000, scale_noise=0.0)
+    last = last[0]
+    alpha = torch.rand(K, device="cuda") + 0.5
+    lr = 0.05
+    delta = torch.empty(ld, device="cuda")
+    sq = torch.zeros(K, dtype=torch.float64, device="cuda")
+    kx.qfed_accumulate(x, K, P, last=last, alpha=alpha, lr=lr, delta=delta, sqnorm=sq,
+                       workspace=kx.qfed_workspace(K, "cuda"), accumulate=False)
+    want = None
+    want_sq = []
+    lr32 = torch.tensor(lr, dtype=torch.float32, device="cuda")
+    for k in range(K):
+        g = (last[:P] - x[k, :P]) / lr32
+        t = alpha[k] * g
+        want = t if want is None else want + t
+        want_sq.append(float((g * g).double().sum()))
+        del g, t
+    assert torch.equal(delta[:P], want)
+    np.testing.assert_allclose(sq.cpu().numpy(), np.array(want_sq), rtol=1e-9)

@@ -64,6 +64,8 @@ if [[ $STAGE == policies ]]; then
   done
 fi
 if [[ $STAGE == tuneqf ]]; then
-  timeout -k 10 900 python tools/tune_qfed.py 1000 25000000 3 > $OUT/tune_qf.log 2>&1 || { tail -20 $OUT/tune_qf.log; exit 1; }
-  cat $OUT/tune_qf.log
+  for P in ${QFP:-25000000}; do
+    timeout -k 10 600 python tools/tune_qfed.py ${QFK:-1000} $P 3 > $OUT/tune_qf_$P.log 2>&1 || { tail -20 $OUT/tune_qf_$P.log; exit 1; }
+    cat $OUT/tune_qf_$P.log
+  done
 fi
