@@ -7,7 +7,9 @@ FedAvg (aggregator.py:489-511): out = (sum of the K updates in arrival order) / 
 A "step" is one aggregation round over the resident K x P batch.  With --gpus N (one process per GPU,
 torchrun) every rank owns an equal 25M-parameter shard of an N x 25M-parameter model and reduces its
 K client slices: weak scaling, no data-path collective.  ``value`` counts client updates of one 25M-fp32
-(100 MB) slice across all ranks per second.  --reassemble additionally times the RCCL all-gather that
+(100 MB) slice across all ranks per second.  ``--shard clients`` is the other layout of SURVEY §8e: every
+rank reduces its own K clients of a whole 25M-parameter model, then one RCCL all-reduce of the partial
+sums (inside the timed step) and the replicated finish; ``value`` = N*K client updates per second.  --reassemble additionally times the RCCL all-gather that
 rebuilds the global model for egress (reported as ``reassembly_ms``, not part of ``value``).
 
 Extra objects on the JSON line:
@@ -41,6 +43,10 @@ def parse():
     ap.add_argument("--clients", type=int, default=1000)
     ap.add_argument("--params", type=int, default=25_000_000, help="fp32 parameters per GPU shard")
     ap.add_argument("--policy", default="fedavg", choices=["fedavg", "fedyogi", "fedbuff", "qfedavg"])
+    ap.add_argument("--shard", default="params", choices=["params", "clients"],
+                    help="params: each rank reduces its slice of the model for every client (no data-path "
+                         "collective, bit-exact); clients: each rank reduces its own K clients over the whole "
+                         "model, then one RCCL all-reduce of the partial sums (state.py)")
     ap.add_argument("--reassemble", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample (0 = skip)")
     ap.add_argument("--seed", type=int, default=2024)
@@ -141,7 +147,8 @@ def main():
             dist.init_process_group("gloo")
     from fedscale_amd.state import ShardGroup
 
-    shards = ShardGroup(rank, world)
+    shards = ShardGroup(rank, world, mode=args.shard)
+    cmode = shards.shards_clients
 
     from fedscale_amd import kernels as kx
     from fedscale_amd import synth
@@ -152,7 +159,9 @@ def main():
     x = torch.empty(K, ld, dtype=torch.float32, device=dev)
     synth.fill(x, K, P, seed=args.seed + 7919 * rank)
     out = torch.zeros(ld, dtype=torch.float32, device=dev)
-    denom = float(np.float32(K))
+    acc = torch.zeros(ld, dtype=torch.float32, device=dev) if cmode else None  # client mode: partial chain
+    Kg = K * world if cmode else K  # clients in the round (client mode: every rank brings K)
+    denom = float(np.float32(Kg))
     yogi = None
     if args.policy == "fedyogi":
         yogi = dict(last=torch.zeros(ld, device=dev), m=torch.zeros(ld, device=dev), v=torch.zeros(ld, device=dev),
@@ -161,8 +170,8 @@ def main():
         synth.fill(yogi["last"].view(1, -1), 1, P, seed=args.seed + 1)
     a = None
     if args.policy == "fedbuff":
-        s = [1 / (1 + (k % 6)) ** 0.5 for k in range(K)]
-        a = torch.tensor(np.asarray(s, dtype=np.float32), device=dev)
+        s = [1 / (1 + (k % 6)) ** 0.5 for k in range(Kg)]
+        a = torch.tensor(np.asarray(s[rank * K:(rank + 1) * K] if cmode else s, dtype=np.float32), device=dev)
         denom = float(np.float32(sum(s)))
     gathered = None
     qf = None
@@ -170,15 +179,16 @@ def main():
         if K > kx.qfed_max_chunk():
             raise SystemExit(f"--policy qfedavg: K <= {kx.qfed_max_chunk()} per chunk in this bench")
         rng = np.random.default_rng(args.seed)
-        losses = rng.uniform(0.5, 2.0, size=K)
+        losses = rng.uniform(0.5, 2.0, size=Kg)
         lr, q = 0.05, 1.0
+        mine = losses[rank * K:(rank + 1) * K] if cmode else losses
         qf = dict(last=torch.empty(1, ld, device=dev), delta=torch.zeros(ld, device=dev),
-                  sq=torch.zeros(K, dtype=torch.float64, device=dev), ws=kx.qfed_workspace(K, dev),
+                  sq=torch.zeros(Kg, dtype=torch.float64, device=dev), ws=kx.qfed_workspace(K, dev),
                   hs=torch.zeros(2, device=dev), lr=lr,
-                  alpha=torch.tensor([np.float32(np.float_power(l + 1e-10, q)) for l in losses], device=dev),
+                  alpha=torch.tensor([np.float32(np.float_power(l + 1e-10, q)) for l in mine], device=dev),
                   c1=torch.tensor([np.float32(q * np.float_power(l + 1e-10, q - 1)) for l in losses], device=dev),
                   c2=torch.tensor([np.float32((1 / lr) * np.float_power(l + 1e-10, q)) for l in losses], device=dev))
-        synth.fill(qf["last"], 1, P, seed=args.seed + 7919 * rank, scale_noise=0.0)
+        synth.fill(qf["last"], 1, P, seed=args.seed + (0 if cmode else 7919 * rank), scale_noise=0.0)
         qf["last"] = qf["last"][0]
 
     stream = torch.cuda.current_stream(dev)
@@ -188,12 +198,28 @@ def main():
             ev[0].record(stream)
         if qf is not None:  # optimizers.py:73-104: phase 1 (timed as the dominant kernel), hs, phase 2
             qf["sq"].zero_()
+            k0 = rank * K if cmode else 0
             kx.qfed_accumulate(x, K, P, last=qf["last"], alpha=qf["alpha"], lr=qf["lr"], delta=qf["delta"],
-                               sqnorm=qf["sq"], workspace=qf["ws"], accumulate=False)
+                               sqnorm=qf["sq"][k0:k0 + K], workspace=qf["ws"], accumulate=False)
             if ev is not None:
                 ev[1].record(stream)
-            kx.qfed_hs(qf["sq"], qf["c1"], qf["c2"], K, qf["hs"])
+            if cmode:  # per-rank partial delta chains + each client's norm from its owner rank
+                shards.all_reduce_sum(qf["delta"])
+                shards.all_reduce_sum(qf["sq"])
+            elif world > 1:
+                shards.all_reduce_sum(qf["sq"])
+            kx.qfed_hs(qf["sq"], qf["c1"], qf["c2"], Kg, qf["hs"])
             kx.qfed_finalize(qf["last"], qf["delta"], qf["hs"], out, P)
+            return
+        if cmode:  # partial chain of this rank's clients, RCCL all-reduce, finish on the summed vector
+            kx.reduce(x, K, P, acc, a=a)
+            if ev is not None:
+                ev[1].record(stream)
+            shards.all_reduce_sum(acc)
+            if yogi is None:
+                kx.reduce(acc.view(1, ld), 1, P, out, denom=denom, finalize=True)
+            else:
+                kx.reduce_yogi(acc.view(1, ld), 1, P, out=out, denom=denom, **yogi)
             return
         if yogi is None:
             kx.reduce(x, K, P, out, a=a, denom=denom, finalize=True)
@@ -240,7 +266,8 @@ def main():
     if rank == 0:
         ms_per_step = wall * 1e3 / args.steps
         value = world * K * args.steps / wall
-        extra = {"fedavg": 0, "fedbuff": 4 * K, "fedyogi": 20 * P, "qfedavg": 4 * P + 8 * K}[args.policy]
+        extra = {"fedavg": 0, "fedbuff": 4 * K, "fedyogi": 0 if cmode else 20 * P,
+                 "qfedavg": 4 * P + 8 * K}[args.policy]
         alg_bytes = 4 * K * P + 4 * P + extra  # SURVEY §8d algorithmic bytes per launch (per GPU)
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
@@ -260,17 +287,21 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32",
             "data": "synthetic full-weight client updates (base + noise, hash-generated on device), HBM-resident",
-            "config": {"workload": f"{args.policy}_k{K}_p{P}_per_gpu", "clients": K, "params_per_gpu": P,
-                       "model_params_total": P * world, "policy": args.policy,
-                       "parallelism": f"param-shard x{world} (one process per GPU)"},
+            "config": ({"workload": f"{args.policy}_k{K}_p{P}_per_gpu", "clients": K, "params_per_gpu": P,
+                        "model_params_total": P * world, "policy": args.policy,
+                        "parallelism": f"param-shard x{world} (one process per GPU)"} if not cmode else
+                       {"workload": f"{args.policy}_k{K}_per_gpu_p{P}_clientshard", "clients": Kg,
+                        "clients_per_gpu": K, "params": P, "model_params_total": P, "policy": args.policy,
+                        "parallelism": f"client-shard x{world} + RCCL all-reduce (one process per GPU)"}),
             "hbm_gbps": achieved,
             "kernel_ms": kern_ms,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": {"fedavg": "k_reduce (fa_reduce FA_FINALIZE)",
-                                    "fedbuff": "k_reduce weighted (fa_reduce FA_FINALIZE)",
-                                    "fedyogi": "k_reduce EPI_YOGI (fa_reduce_yogi)",
-                                    "qfedavg": "k_qfed_accum + k_qfed_gather (fa_qfed_accumulate)"}[args.policy],
+                         "kernel": ("k_qfed_accum + k_qfed_gather (fa_qfed_accumulate)" if args.policy == "qfedavg"
+                                    else "k_reduce (fa_reduce, this rank's partial chain)" if cmode else
+                                    {"fedavg": "k_reduce (fa_reduce FA_FINALIZE)",
+                                     "fedbuff": "k_reduce weighted (fa_reduce FA_FINALIZE)",
+                                     "fedyogi": "k_reduce EPI_YOGI (fa_reduce_yogi)"}[args.policy]),
                          "alg_bytes_per_launch": alg_bytes},
         }
         if reassembly_ms is not None:

@@ -47,7 +47,10 @@ class TorchModelAdapter(ModelAdapterBase):
         self.device = _resolve_device(device)
         self.shards = shards or ShardGroup()
         sd = model.state_dict()
-        self.layout = BucketLayout.from_state_dict(sd, self.shards.rank, self.shards.world)
+        if self.shards.shards_params:
+            self.layout = BucketLayout.from_state_dict(sd, self.shards.rank, self.shards.world)
+        else:  # single GPU, or client mode: every rank holds the whole model
+            self.layout = BucketLayout.from_state_dict(sd)
         L, dev = self.layout, self.device
         self._f = [torch.zeros(L.ld, dtype=torch.float32, device=dev) for _ in range(2)]
         self._s = [torch.zeros(L.ldq, dtype=torch.int64, device=dev) for _ in range(2)]
@@ -79,7 +82,7 @@ class TorchModelAdapter(ModelAdapterBase):
         self._version += 1
 
     def _sqnorm_allreduce(self):
-        return self.shards.all_reduce_sum if self.shards.world > 1 else None
+        return self.shards.all_reduce_sum if self.shards.shards_params else None
 
     def _pack_values(self, values: list, f_dst: torch.Tensor, s_dst: torch.Tensor):
         """weights list -> device fp32 bucket slice + side table (converted to s_dst's dtype)."""
@@ -150,13 +153,18 @@ class TorchModelAdapter(ModelAdapterBase):
     # ---- device fast path -----------------------------------------------------------------------
     def begin_round(self, K: int, policy: str, capacity: Optional[int] = None) -> DeviceRound:
         cap = capacity or self.staging_capacity
-        want = min(cap or default_capacity(self.layout, K, self.device), K)
+        K_local = K
+        if self.shards.shards_clients:  # this rank stages only its block of the arrivals
+            k0, k1 = self.shards.client_block(K)
+            K_local = max(1, k1 - k0)
+        want = min(cap or default_capacity(self.layout, K_local, self.device), K_local)
         if self.staging is None or self.staging.capacity < want:
             self.staging = None
             self.staging = ClientStaging(self.layout, self.device, want)
         snap = self._snapshot()
         return DeviceRound(self.layout, self.device, K, policy, capacity=want, staging=self.staging,
-                           last_f32=snap.f32, last_i64=snap.side)
+                           last_f32=snap.f32, last_i64=snap.side,
+                           clients=self.shards if self.shards.shards_clients else None)
 
     def apply_round(self, rnd: DeviceRound, denom32: float, denom64: float, client_training_results=None,
                     keep_mean: bool = True):

@@ -7,6 +7,11 @@ staged into a [capacity, ld] device buffer; whenever it fills before the round e
 folded into the running state by one kernel launch (the same per-element chain continues, so chunking
 never changes a bit of the result).  The last chunk is reduced by ``finalize_*`` with the server step
 fused in.
+
+With a client-mode ``ShardGroup`` (``state.py``) the round is spread over ranks by arrival index: each
+rank stages and folds only its own contiguous block of arrivals (its chain starts from its first client),
+the partial chains / q-FedAvg deltas / side-table sums meet in one RCCL all-reduce, and the finishing
+epilogue (divide, fused FedYoGi, q-FedAvg hs + step) runs replicated on the summed vector.
 """
 from __future__ import annotations
 
@@ -17,6 +22,7 @@ import torch
 
 from . import kernels as kx
 from .bucket import BucketLayout, ClientStaging
+from .state import ShardGroup
 
 POLICIES = ("fedavg", "fedbuff", "qfedavg")
 
@@ -36,24 +42,31 @@ def default_capacity(layout: BucketLayout, K: int, device, budget_fraction: floa
 class DeviceRound:
     def __init__(self, layout: BucketLayout, device, K: int, policy: str, *, capacity: Optional[int] = None,
                  staging: Optional[ClientStaging] = None, last_f32: Optional[torch.Tensor] = None,
-                 last_i64: Optional[torch.Tensor] = None):
+                 last_i64: Optional[torch.Tensor] = None, clients: Optional[ShardGroup] = None):
         if policy not in POLICIES:
             raise ValueError(f"policy {policy!r} not in {POLICIES}")
         if K < 1:
             raise ValueError("a round needs K >= 1 client results")
         self.layout, self.device, self.K, self.policy = layout, torch.device(device), int(K), policy
+        self.cg = clients if clients is not None and clients.shards_clients else None
+        if self.cg is not None and layout.world != 1:
+            raise ValueError("client-mode rounds need the unsharded (whole-model) layout")
+        # [k_begin, k_end): the arrival indices this rank reduces (all of them unless client-sharded)
+        self.k_begin, self.k_end = self.cg.client_block(self.K) if self.cg is not None else (0, self.K)
+        K_local = max(1, self.k_end - self.k_begin)
         if policy == "qfedavg":
             qmax = kx.qfed_max_chunk()
             capacity = min(capacity or qmax, qmax)
-        if staging is not None and (capacity is None or staging.capacity >= min(capacity, K)):
+        if staging is not None and (capacity is None or staging.capacity >= min(capacity, K_local)):
             self.staging = staging
         else:
-            cap = capacity or default_capacity(layout, K, self.device)
-            self.staging = ClientStaging(layout, self.device, min(cap, K))
+            cap = capacity or default_capacity(layout, K_local, self.device)
+            self.staging = ClientStaging(layout, self.device, min(cap, K_local))
         self.cap = min(self.staging.capacity, capacity or self.staging.capacity)
         self.staging.generation += 1  # a new round takes the staging slots over
         self.generation = self.staging.generation
-        self.n = 0  # results received
+        self.n = 0  # results received (all ranks' arrivals)
+        self.n_local = 0  # results staged by this rank
         self.slot = 0  # staged in the current chunk
         self.chunks_done = 0
         dev, L = self.device, layout
@@ -82,6 +95,11 @@ class DeviceRound:
         """Stage one arriving client update (in arrival order)."""
         if self.n >= self.K:
             raise RuntimeError(f"round already has its K={self.K} results")
+        if not (self.k_begin <= self.n < self.k_end):  # another rank's client (client mode)
+            if self.policy == "qfedavg":
+                self._qfed_scalars(self.n, loss, learning_rate, q)  # hs needs every client's scalars
+            self.n += 1
+            return
         if self.slot == self.cap:
             self._fold_chunk()
         self.staging.put(self.slot, update)
@@ -92,6 +110,7 @@ class DeviceRound:
             self._qfed_scalars(self.n, loss, learning_rate, q)
         self.slot += 1
         self.n += 1
+        self.n_local += 1
 
     def _qfed_scalars(self, k, loss, lr, q):
         """Per-client scalars of optimizers.py:87-98, computed in double exactly as the reference does."""
@@ -125,7 +144,7 @@ class DeviceRound:
             kx.side_accumulate(st.xi, n, L.Q, 0 if self.policy == "fedavg" else 1, w=a64, acc_i=self.acc_i,
                                acc_d=self.acc_d, accumulate=not first)
         else:
-            k0 = self.n - n
+            k0 = self.k_begin + self.n_local - n  # arrival index of the chunk's first client
             alpha = torch.from_numpy(self.alpha[k0:k0 + n].copy()).to(self.device, non_blocking=True)
             if L.P > 0:
                 kx.qfed_accumulate(st.x, n, L.P, last=self.last_f32, alpha=alpha, lr=self.lr, delta=self.delta,
@@ -139,6 +158,27 @@ class DeviceRound:
         if self.n != self.K:
             raise RuntimeError(f"finalize with {self.n} of K={self.K} results")
 
+    def _cross_rank_sum(self, *tensors):
+        """Client mode: sum the per-rank partials (RCCL all-reduce over xGMI).  A rank that reduced no
+        client contributes zeros."""
+        for t in tensors:
+            self.cg.all_reduce_sum(t)
+
+    def _finalize_mean_clients(self, denom32, denom64, out, cur_side, model_side, yogi):
+        L = self.layout
+        if self.slot:
+            self._fold_chunk()
+        if self.acc is None:
+            self.acc = torch.zeros(L.ld, dtype=torch.float32, device=self.device)
+        mode = 0 if self.policy == "fedavg" else 1
+        self._cross_rank_sum(self.acc, self.acc_i if mode == 0 else self.acc_d)
+        x1 = self.acc.view(1, L.ld)  # the summed chain as a one-client chunk: out = 1*sum / denom
+        if yogi is None:
+            kx.reduce(x1, 1, L.P, out, denom=denom32, finalize=True)
+        else:
+            kx.reduce_yogi(x1, 1, L.P, denom=denom32, out=out, **yogi)
+        kx.side_close(L.Q, mode, denom64, acc_i=self.acc_i, acc_d=self.acc_d, cur=cur_side, model=model_side)
+
     # ---- FedAvg / FedBuff: mean (+ optional fused FedYoGi) --------------------------------------
     def finalize_mean(self, denom32: float, denom64: float, *, out: torch.Tensor, cur_side: torch.Tensor,
                       model_side: Optional[torch.Tensor] = None, yogi: Optional[dict] = None):
@@ -150,6 +190,8 @@ class DeviceRound:
         yogi       -> dict(last=, m=, v=, eta=, tau=, beta=, omb=, omb2=, init=)
         """
         self._check_complete()
+        if self.cg is not None:
+            return self._finalize_mean_clients(denom32, denom64, out, cur_side, model_side, yogi)
         L, st, n = self.layout, self.staging, self.slot
         first = self.chunks_done == 0
         a32 = a64 = None
@@ -168,6 +210,8 @@ class DeviceRound:
         """The plain FedAvg mean of this round (aggregator.py:497-507), recomputed from the staged updates
         when they are all still resident (q-FedAvg rounds do not need it, but the reference keeps it in
         ``Aggregator.model_weights``).  Returns False when the staging was folded or reused."""
+        if self.cg is not None:
+            return False  # client mode: each rank holds only its block of the updates
         if self.cap < self.K or self.staging.generation != self.generation or self.n != self.K:
             return False  # some updates were overwritten by later chunks, or the slots were reused
         L, st = self.layout, self.staging
@@ -187,7 +231,11 @@ class DeviceRound:
         L = self.layout
         if self.slot:
             self._fold_chunk()
-        if sqnorm_allreduce is not None:
+        if self.cg is not None:
+            # each client's norms were computed on its owner rank only: the sum is a gather (exact);
+            # delta and delta_s are per-rank partial chains
+            self._cross_rank_sum(self.delta, self.delta_s, self.sqnorm, self.sqnorm_side)
+        elif sqnorm_allreduce is not None:
             sqnorm_allreduce(self.sqnorm)
         # side table: replicated on every rank, so it is added once, after the cross-shard sum
         self.sqnorm += self.sqnorm_side

@@ -4,9 +4,18 @@
 ``f32`` is this rank's slice of the fp32 bucket, ``side`` the replicated side table (int64 for a model
 state, float64 for a FedAvg mean of int64 entries).
 
-Sharding (one process per GPU, torch.distributed over RCCL): every rank owns an equal-size slice of the
-fp32 bucket, so the only collectives the path needs are the all-gather that reassembles the global model
-for egress and, for q-FedAvg, one all-reduce of the K per-client squared norms.
+Two ways to spread a round over the GPUs of a node (one process per GPU, torch.distributed over RCCL;
+SURVEY §8e):
+
+* ``mode="params"`` (default): every rank owns an equal-size slice of the fp32 bucket and reduces its
+  slice of every client update.  The only collectives are the all-gather that reassembles the global model
+  for egress and, for q-FedAvg, one all-reduce of the K per-client squared norms.  The per-element chain
+  is the reference's, so the result is bit-exact.
+* ``mode="clients"``: every rank holds the whole model and reduces a contiguous block of the round's
+  arrivals (rank r takes arrival indices [r*K/N, (r+1)*K/N)).  The per-rank partial sums meet in one RCCL
+  all-reduce (the "final RCCL reduce" of the north star) and the server step then runs replicated, so
+  egress needs no gather.  Summing per-rank partials re-associates the fp32 chain: the result is within
+  the north-star tolerance (1e-5 relative), not bit-exact; int64 side-table sums stay exact.
 """
 from __future__ import annotations
 
@@ -25,19 +34,43 @@ class FlatState:
     side: torch.Tensor
 
 
-class ShardGroup:
-    """rank/world of the model shards; ``None`` group = single GPU, no collectives."""
+MODES = ("params", "clients")
 
-    def __init__(self, rank: int = 0, world: int = 1, group=None):
-        self.rank, self.world, self.group = rank, world, group
+
+class ShardGroup:
+    """rank/world of the GPUs sharing a round; ``None`` group = the default process group."""
+
+    def __init__(self, rank: int = 0, world: int = 1, group=None, mode: str = "params"):
+        if mode not in MODES:
+            raise ValueError(f"shard mode {mode!r} not in {MODES}")
+        self.rank, self.world, self.group, self.mode = rank, world, group, mode
 
     @classmethod
-    def from_env(cls, group=None) -> "ShardGroup":
+    def from_env(cls, group=None, mode: str = "params") -> "ShardGroup":
         import torch.distributed as dist
 
         if dist.is_available() and dist.is_initialized():
-            return cls(dist.get_rank(group), dist.get_world_size(group), group)
-        return cls()
+            return cls(dist.get_rank(group), dist.get_world_size(group), group, mode)
+        return cls(mode=mode)
+
+    @property
+    def shards_params(self) -> bool:
+        """The fp32 bucket is split across ranks (egress needs the all-gather)."""
+        return self.world > 1 and self.mode == "params"
+
+    @property
+    def shards_clients(self) -> bool:
+        """Each rank reduces a block of the round's clients over the whole model."""
+        return self.world > 1 and self.mode == "clients"
+
+    def client_block(self, K: int, rank: Optional[int] = None):
+        """[k0, k1): the arrival indices rank ``rank`` reduces in client mode (contiguous, balanced)."""
+        r = self.rank if rank is None else rank
+        return r * K // self.world, (r + 1) * K // self.world
+
+    def owner(self, k: int, K: int) -> int:
+        """The rank that reduces arrival index k of a K-client round (client mode)."""
+        return ((k + 1) * self.world - 1) // K
 
     def _host_staged(self, t: torch.Tensor) -> bool:
         """gloo (CPU tests, several ranks sharing one GPU) moves device tensors through the host."""
@@ -46,8 +79,9 @@ class ShardGroup:
         return t.device.type == "cuda" and dist.get_backend(self.group) == "gloo"
 
     def all_gather(self, shard: torch.Tensor) -> torch.Tensor:
-        """Concatenate the equal-size shards of every rank (RCCL all-gather over xGMI)."""
-        if self.world == 1:
+        """Concatenate the equal-size shards of every rank (RCCL all-gather over xGMI).  In client mode the
+        model is replicated, so the local copy already is the whole model."""
+        if not self.shards_params:
             return shard
         import torch.distributed as dist
 

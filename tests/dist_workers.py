@@ -51,9 +51,46 @@ def cpu_shard_worker(rank, world, port, name):
         dist.destroy_process_group()
 
 
-def gpu_shard_worker(rank, world, port, name, capacity):
-    """The full device path with the model sharded over `world` ranks (all on cuda:0, gloo for the
-    collectives): per-shard kernels, q-FedAvg norm all-reduce, all-gather reassembly on egress."""
+def cpu_client_shard_worker(rank, world, port, name):
+    """Client mode on CPU: every rank reduces its contiguous block of arrivals with the oracle chain, the
+    all-reduced partial chains / K equal the unsharded FedAvg mean within fp32 re-association error, and
+    the int64 side-table sums are exact."""
+    from fedscale_amd.bucket import BucketLayout
+    from fedscale_amd.state import ShardGroup
+    from oracle.cpu_reference import fedavg_flat
+    from tests.golden_io import Scenario
+
+    _init(rank, world, port)
+    try:
+        sc = Scenario(name)
+        dtypes = [getattr(torch, d) for d in sc.meta["dtypes"]]
+        full = BucketLayout(sc.names, sc.meta["shapes"], dtypes)
+        K = sc.meta["rounds"][0]
+        g = ShardGroup(rank, world, mode="clients")
+        k0, k1 = g.client_block(K)
+        assert all(g.owner(k, K) == rank for k in range(k0, k1))
+        xf = np.zeros((K, full.ld), np.float32)
+        xi = np.zeros((K, full.ldq), np.int64)
+        for k in range(K):
+            full.pack_host(full.values_of(sc.client(k)), xf[k], xi[k])
+        part = np.zeros(full.ld, np.float32)
+        for k in range(k0, k1):  # the rank's own chain, from its first client
+            part = xf[k].copy() if k == k0 else part + xf[k]
+        tot = g.all_reduce_sum(torch.from_numpy(part)).numpy() / np.float32(K)
+        want = fedavg_flat(xf)
+        np.testing.assert_allclose(tot[:full.P_full], want[:full.P_full], rtol=1e-5,
+                                   atol=1e-6 * float(np.abs(want).max() + 1e-30))
+        side = g.all_reduce_sum(torch.from_numpy(xi[k0:k1].sum(axis=0))).numpy()
+        np.testing.assert_array_equal(side, xi.sum(axis=0))
+    finally:
+        dist.destroy_process_group()
+
+
+def gpu_shard_worker(rank, world, port, name, capacity, mode="params"):
+    """The full device path with the round spread over `world` ranks (all on cuda:0, gloo for the
+    collectives).  mode "params": per-shard kernels, q-FedAvg norm all-reduce, all-gather reassembly on
+    egress (bit-exact).  mode "clients": per-rank blocks of arrivals, all-reduced partials, replicated
+    server step (within the north-star tolerance)."""
     from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator, DeviceAsyncAggregator
     from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
     from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
@@ -68,7 +105,7 @@ def gpu_shard_worker(rank, world, port, name, capacity):
         opt = (TorchServerOptimizer(args.gradient_policy, args, "cuda:0")
                if sc.meta.get("optimizer") is not None else None)
         adapter = TorchModelAdapter(StateDictModule(sc.names, sc.init_state()), optimizer=opt, device="cuda:0",
-                                    shards=ShardGroup(rank, world), staging_capacity=capacity)
+                                    shards=ShardGroup(rank, world, mode=mode), staging_capacity=capacity)
         policy = sc.meta["policy"]
         if policy == "fedbuff":
             agg = DeviceAsyncAggregator(adapter, args)
@@ -84,7 +121,10 @@ def gpu_shard_worker(rank, world, port, name, capacity):
             for res in sc.results(ks, r):
                 agg.on_result(res)
             got = adapter.get_weights()
-            if policy == "q-fedavg":
+            if mode == "clients":  # re-associated fp32 sums; int64 FedAvg sums stay exact
+                assert_state_close(got, sc.expected(r), 1e-5, f"{name} clients rank{rank} r{r}",
+                                   int_slack=0 if policy == "fedavg" and opt is None else 1)
+            elif policy == "q-fedavg":
                 assert_state_close(got, sc.expected(r), 1e-5, f"{name} rank{rank} r{r}", int_slack=1)
             elif policy == "fed-yogi":
                 assert_state_close(got, sc.expected(r), 1e-6, f"{name} rank{rank} r{r}")

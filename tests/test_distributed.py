@@ -26,7 +26,19 @@ def test_cpu_sharded_reduction_world3(name):
     mp.spawn(dist_workers.cpu_shard_worker, args=(3, _port(), name), nprocs=3, join=True)
 
 
+@pytest.mark.parametrize("name,world", [("fedavg_femnist_cnn_k10", 2), ("fedavg_mixed_k7", 2),
+                                        ("fedavg_wide_k64", 2), ("fedavg_mixed_k3", 3), ("fedavg_wide_k64", 4)])
+def test_cpu_client_sharded_reduction(name, world):
+    mp.spawn(dist_workers.cpu_client_shard_worker, args=(world, _port(), name), nprocs=world, join=True)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", [n for n in scenario_names() if n != "kat_linear_225"])
 def test_gpu_sharded_device_path_world2(gpu_device, name):
     mp.spawn(dist_workers.gpu_shard_worker, args=(2, _port(), name, 2), nprocs=2, join=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", [n for n in scenario_names() if n != "kat_linear_225"])
+def test_gpu_client_sharded_device_path_world2(gpu_device, name):
+    mp.spawn(dist_workers.gpu_shard_worker, args=(2, _port(), name, 2, "clients"), nprocs=2, join=True)

@@ -52,6 +52,12 @@ if [[ $STAGE == dist ]]; then
   tail -3 $OUT/pytest_dist.log
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 1 --clients 100 --params 4000000 --dist-backend gloo --reassemble > $OUT/bench_dist2.log 2>&1 || { tail -30 $OUT/bench_dist2.log; exit 1; }
   grep '^{' $OUT/bench_dist2.log
+  for pol in fedavg fedyogi qfedavg; do
+    timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 1 --clients 100 --params 4000000 --dist-backend gloo --shard clients --policy $pol > $OUT/bench_dist2_clients_$pol.log 2>&1 || { tail -30 $OUT/bench_dist2_clients_$pol.log; exit 1; }
+    grep '^{' $OUT/bench_dist2_clients_$pol.log
+  done
+  timeout -k 10 300 python bench.py --shard clients --steps 5 --warmup 1 --cpu-seconds 0 --no-other-configs > $OUT/bench_clients_n1.log 2>&1 || { tail -30 $OUT/bench_clients_n1.log; exit 1; }
+  grep '^{' $OUT/bench_clients_n1.log
 fi
 if [[ $STAGE == ingress ]]; then
   timeout -k 10 600 python tools/ingress_bench.py 200 3 resnet18 ${WORKERS:-1,4,8,16} > $OUT/ingress.log 2>&1 || { tail -30 $OUT/ingress.log; exit 1; }
