@@ -1,4 +1,4 @@
-"""ctypes binding of libfedagg.so — the C ABI declared in include/fedagg.h.
+"""ctypes binding of libfedagg.so — the C ABI declared in include/fedagg.h and include/fedclient.h.
 
 This is the only way the package reaches the GPU.  There is no fallback: if the shared library is
 missing or a call fails, a ``FedAggError`` is raised.  Build it with ``python __graft_entry__.py``
@@ -17,6 +17,8 @@ ABI_VERSION = 1
 FA_ACCUMULATE = 1
 FA_FINALIZE = 2
 FA_YOGI_INIT = 4
+FA_DP_WRITE_PARAM = 1
+FA_DP_SCALE_ONLY = 2
 
 
 class FedAggError(RuntimeError):
@@ -26,7 +28,7 @@ class FedAggError(RuntimeError):
 _c_void_p, _i32, _i64, _f32, _f64, _u32 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_float,
                                              ctypes.c_double, ctypes.c_uint32)
 
-# name -> (restype, argtypes);  must list every symbol of include/fedagg.h
+# name -> (restype, argtypes);  must list every symbol of include/fedagg.h and include/fedclient.h
 SIGNATURES = {
     "fa_abi_version": (_i32, []),
     "fa_last_error_string": (ctypes.c_char_p, []),
@@ -53,6 +55,15 @@ SIGNATURES = {
     "fa_host_gather": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32]),
     "fa_prefix_box_combine": (_i32, [_c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _i32,
                                      _c_void_p, _c_void_p]),
+    # include/fedclient.h (client-side handlers; pointer tables are host arrays)
+    "fa_prox_update": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _f32, _c_void_p]),
+    "fa_dp_workspace_bytes": (_i64, [_c_void_p, _i32]),
+    "fa_dp_clip_coef": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _f32, _i32, _c_void_p, _c_void_p,
+                               _c_void_p]),
+    "fa_dp_apply": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _f32,
+                           ctypes.c_uint64, _i32, _c_void_p]),
+    "fa_dp_noise_i64": (_i32, [_c_void_p, _c_void_p, _i64, _f32, ctypes.c_uint64, _i64, _c_void_p]),
+    "fa_dp_normals": (_i32, [_c_void_p, _i64, ctypes.c_uint64, _i64, _c_void_p]),
 }
 
 _lib = None

@@ -53,6 +53,12 @@ static int check_launch(const char* what) {
 }
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
+// shared with the other translation units of the library (client_update.hip)
+extern "C" __attribute__((visibility("hidden"))) int fa_internal_set_error(int code, const char* msg) {
+  snprintf(g_err, sizeof(g_err), "%s", msg);
+  return code;
+}
+
 extern "C" int fa_abi_version(void) { return FA_ABI_VERSION; }
 extern "C" const char* fa_last_error_string(void) { return g_err; }
 

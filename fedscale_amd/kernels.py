@@ -178,3 +178,105 @@ def fill_synthetic(x: torch.Tensor, K: int, P: int, *, seed: int, k0: int = 0, s
     call("fa_fill_synthetic", ptr(x), ld, K, P, seed & 0xFFFFFFFF, k0, float(scale_base), float(scale_noise),
          _stream(x))
     return x
+
+
+# ---- client-side handlers (include/fedclient.h): multi-tensor launches over HOST pointer tables -----
+class _Table:
+    """Host arrays of device pointers / element counts for one tensor list (kept alive for the call)."""
+
+    def __init__(self, lists, numel):
+        import numpy as np
+
+        self.arrays = []
+        for lst in lists:
+            if lst is None:
+                self.arrays.append(None)
+                continue
+            self.arrays.append(np.asarray([0 if t is None else t.data_ptr() for t in lst], dtype=np.uint64))
+        self.numel = np.asarray(numel, dtype=np.int64)
+
+    def ptr(self, i):
+        a = self.arrays[i]
+        return None if a is None else a.ctypes.data
+
+
+def _fp32_list(ts, name, device=None, allow_none=False):
+    dev = device
+    for i, t in enumerate(ts):
+        if t is None and allow_none:
+            continue
+        _dev(t, torch.float32, f"{name}[{i}]", align=4)
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError(f"{name}[{i}]: on {t.device}, expected {dev}")
+    return dev
+
+
+def prox_update(params, global_model, c: float):
+    """param[t] += c * (param[t] - global[t]) for every tensor, one multi-tensor launch (fa_prox_update)."""
+    params, global_model = list(params), list(global_model)
+    if len(params) != len(global_model):
+        raise ValueError(f"{len(params)} parameters but {len(global_model)} global tensors")
+    if not params:
+        return
+    dev = _fp32_list(params, "param")
+    _fp32_list(global_model, "global_model", dev)
+    for i, (p, g) in enumerate(zip(params, global_model)):
+        if p.shape != g.shape:
+            raise ValueError(f"param[{i}] shape {tuple(p.shape)} != global_model[{i}] shape {tuple(g.shape)}")
+    tab = _Table([params, global_model], [p.numel() for p in params])
+    call("fa_prox_update", tab.ptr(0), tab.ptr(1), tab.numel.ctypes.data, len(params), float(c),
+         _stream(params[0]))
+
+
+def dp_clip_coef(params, last, max_norm: float, norm_inf: bool, coef_out: torch.Tensor):
+    """coef_out[0:3] <- (total norm of param - last, clip coefficient, apply flag) (fa_dp_clip_coef)."""
+    params = list(params)
+    last = list(last) if last is not None else [None] * len(params)
+    dev = _fp32_list(params, "param", coef_out.device)
+    _fp32_list(last, "last", dev, allow_none=True)
+    _dev(coef_out, torch.float32, "coef_out", 3, align=4)
+    tab = _Table([params, last], [p.numel() for p in params])
+    nbytes = N.load().fa_dp_workspace_bytes(tab.numel.ctypes.data, len(params))
+    ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=dev)
+    call("fa_dp_clip_coef", tab.ptr(0), tab.ptr(1), tab.numel.ctypes.data, len(params), float(max_norm),
+         1 if norm_inf else 0, ptr(ws), ptr(coef_out), _stream(coef_out))
+    return ws  # keep alive until the stream has consumed it (caller holds the reference)
+
+
+def dp_apply(params, last, upload, noise_offset, coef: torch.Tensor, sigma: float, seed: int,
+             write_param: bool = True, scale_only: bool = False):
+    """Recover (+ clip) and noise every tensor in one multi-tensor launch (fa_dp_apply)."""
+    import numpy as np
+
+    params = list(params)
+    T = len(params)
+    last = list(last) if last is not None else [None] * T
+    dev = _fp32_list(params, "param", coef.device)
+    _fp32_list(last, "last", dev, allow_none=True)
+    _dev(coef, torch.float32, "coef", 3, align=4)
+    if not scale_only:
+        upload = list(upload)
+        _fp32_list(upload, "upload", dev)
+        for i, (p, u) in enumerate(zip(params, upload)):
+            if u.numel() != p.numel():
+                raise ValueError(f"upload[{i}] has {u.numel()} elements, param has {p.numel()}")
+    tab = _Table([params, last, None if scale_only else upload], [p.numel() for p in params])
+    offs = np.asarray(noise_offset if noise_offset is not None else [0] * T, dtype=np.int64)
+    flags = (N.FA_DP_WRITE_PARAM if write_param else 0) | (N.FA_DP_SCALE_ONLY if scale_only else 0)
+    call("fa_dp_apply", tab.ptr(0), tab.ptr(1), tab.ptr(2), tab.numel.ctypes.data, offs.ctypes.data, T, ptr(coef),
+         float(sigma), int(seed) & 0xFFFFFFFFFFFFFFFF, flags, _stream(coef))
+
+
+def dp_noise_i64(x: torch.Tensor, out: torch.Tensor, sigma: float, seed: int, noise_offset: int):
+    _dev(x, torch.int64, "x", align=8)
+    _dev(out, torch.float64, "out", x.numel(), align=8)
+    call("fa_dp_noise_i64", ptr(x), ptr(out), x.numel(), float(sigma), int(seed) & 0xFFFFFFFFFFFFFFFF,
+         int(noise_offset), _stream(x))
+
+
+def dp_normals(out: torch.Tensor, seed: int, noise_offset: int = 0):
+    _dev(out, torch.float32, "out", align=4)
+    call("fa_dp_normals", ptr(out), out.numel(), int(seed) & 0xFFFFFFFFFFFFFFFF, int(noise_offset), _stream(out))
+    return out

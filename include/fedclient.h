@@ -1,0 +1,77 @@
+/*
+ * fedclient.h — C ABI of the client-side element-wise weight handlers on MI355X (gfx950), SURVEY §8f
+ * row 4.  Built into the same libfedagg.so as fedagg.h and following its conventions (0 / negative FA_E*
+ * codes, fa_last_error_string(), asynchronous on `stream`, caller-owned device memory, stateless).
+ *
+ * A model is a list of T separately allocated tensors: every entry point takes HOST arrays of T device
+ * pointers and element counts and processes the whole list in a few multi-tensor launches (the table
+ * travels in the kernel arguments).  Pointers must be 4-byte aligned; 16-byte aligned tensors take the
+ * float4 path.
+ *
+ * The reference runs these handlers in the executor, on whatever device trains the model; there is no
+ * native code or FFI on this path, so the "interface" replaced is the Python function cited per entry
+ * point (fedscale_amd/cloud/execution/ binds them through ctypes).
+ */
+#ifndef FEDCLIENT_H
+#define FEDCLIENT_H
+
+#include <stdint.h>
+
+#include "fedagg.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* flags of fa_dp_apply */
+enum {
+  FA_DP_WRITE_PARAM = 1, /* also store the recovered parameter last + clip(delta) back into param[t] */
+  FA_DP_SCALE_ONLY = 2,  /* clip_grad_norm_ alone: param[t] *= coef when coef < 1; no upload, no noise */
+};
+
+/*
+ * FedProx proximal step, fedscale/cloud/execution/optimizers.py:6-10 (ClientOptimizer.update_client_weight,
+ * called after every local step at torch_client.py:238-240):
+ *   param[t][i] = param[t][i] + c * (param[t][i] - global[t][i])     c = fp32(learning_rate * proxy_mu)
+ * every op rounded in fp32 as torch does it (bit-exact).
+ */
+int fa_prox_update(float* const* param, const float* const* global, const int64_t* numel, int32_t T, float c,
+                   fa_stream_t stream);
+
+/*
+ * Local-DP clipping coefficient, examples/differential_privacy/clip_norm.py:12-52 applied to
+ * delta[t] = param[t] - last[t] (customized_client.py:51-55; last[t] == NULL: delta[t] = param[t]):
+ *   norms[t] = ||delta[t]||_2 (fp32)  ->  total = ||stack(norms)||_2   (norm_inf: max |delta|)
+ *   coef = fp32(max_norm) / (total + 1e-6f);  apply = coef < 1
+ * Writes coef_out[0] = total, coef_out[1] = coef, coef_out[2] = apply ? 1 : 0 (device fp32[3]).
+ * Squares are summed in fp64 in a fixed order (deterministic).  workspace: fa_dp_workspace_bytes(numel, T)
+ * bytes of device memory, 8-byte aligned.
+ */
+int64_t fa_dp_workspace_bytes(const int64_t* numel, int32_t T);
+int fa_dp_clip_coef(const float* const* param, const float* const* last, const int64_t* numel, int32_t T,
+                    float max_norm, int32_t norm_inf, void* workspace, float* coef_out, fa_stream_t stream);
+
+/*
+ * Local-DP recover + noise, customized_client.py:57-63, with coef from fa_dp_clip_coef:
+ *   last[t] != NULL (a parameter): d = param - last; if apply: d = d * coef; pn = last + d;
+ *                                  param = pn (FA_DP_WRITE_PARAM); upload = pn + z * sigma
+ *   last[t] == NULL (a buffer):    upload = param + z * sigma
+ * z = N(0,1) from a counter-based generator keyed by (seed, noise_offset[t] + i) — the same distribution
+ * as the reference's torch.normal(mean=0, std=sigma), a different stream; sigma = 0 adds exactly +0.
+ * FA_DP_SCALE_ONLY: param = apply ? param * coef : param (clip_norm.py:50-52 alone; upload/noise unused).
+ */
+int fa_dp_apply(float* const* param, const float* const* last, float* const* upload, const int64_t* numel,
+                const int64_t* noise_offset, int32_t T, const float* coef, float sigma, uint64_t seed, int32_t flags,
+                fa_stream_t stream);
+
+/* int64 state_dict entries: out = double(x) + double(z * sigma)  (numpy int64 + float32 -> float64). */
+int fa_dp_noise_i64(const int64_t* x, double* out, int64_t n, float sigma, uint64_t seed, int64_t noise_offset,
+                    fa_stream_t stream);
+
+/* The generator alone: out[i] = z(seed, noise_offset + i) (for the distribution tests). */
+int fa_dp_normals(float* out, int64_t n, uint64_t seed, int64_t noise_offset, fa_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FEDCLIENT_H */

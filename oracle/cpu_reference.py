@@ -18,6 +18,9 @@ Reference anchors (paths relative to /root/reference):
 * YoGi .............................. fedscale/utils/optimizer/yogi.py:5-36
 * Auxo per-cohort FedAvg ............ examples/auxo/aggregator.py:451-472
 * HeteroFL combine_models ........... examples/heterofl/customized_aggregator.py:78-119
+* FedProx client step ............... fedscale/cloud/execution/optimizers.py:6-10
+* local-DP clip + recover + noise ... examples/differential_privacy/customized_client.py:51-63,
+                                      clip_norm.py:12-52 (pinned by tests/golden/gen_golden_client.py)
 
 Numerics notes (each reproduced deliberately):
 * accumulation is numpy, fp32, strictly in arrival order, allocating a new array each add;
@@ -279,3 +282,60 @@ def fedbuff_flat(x: np.ndarray, s: Sequence[float]) -> np.ndarray:
         acc = acc + s[k] * x[k]
         den += s[k]
     return np.divide(acc, den)
+
+
+# ------------------------------------------------------------------------------------------------
+# client-side element-wise handlers
+# ------------------------------------------------------------------------------------------------
+def fedprox_update(params: Sequence[np.ndarray], global_model: Sequence[np.ndarray], lr: float,
+                   mu: float) -> list:
+    """optimizers.py:10 ``param.data += conf.learning_rate * conf.proxy_mu * (param.data - global_model[idx])``:
+    the Python-double product lr*mu multiplies an fp32 tensor, so it is rounded to fp32 first; every op
+    rounds in fp32."""
+    c = np.float32(lr * mu)
+    return [np.asarray(p, np.float32) + c * (np.asarray(p, np.float32) - np.asarray(g, np.float32))
+            for p, g in zip(params, global_model)]
+
+
+def dp_clip_coef(deltas: Sequence[np.ndarray], max_norm: float, norm_type: float = 2.0):
+    """clip_norm.py:32-52 on CPU tensors, op for op (torch CPU norm, as the reference computes it).
+    Returns (total_norm, clip_coef, apply) as fp32 / bool."""
+    ts = [torch.from_numpy(np.ascontiguousarray(d, dtype=np.float32)) for d in deltas]
+    if len(ts) == 0:
+        return np.float32(0.0), None, False
+    if norm_type == float("inf"):
+        norms = [t.detach().abs().max() for t in ts]
+        total = norms[0] if len(norms) == 1 else torch.max(torch.stack(norms))
+    else:
+        total = torch.norm(torch.stack([torch.norm(t.detach(), norm_type) for t in ts]), norm_type)
+    coef = float(max_norm) / (total + 1e-6)
+    return np.float32(total.item()), np.float32(coef.item()), bool(coef < 1)
+
+
+def dp_privatize(state: "OrderedDict[str, np.ndarray]", is_param: Sequence[bool], last: Sequence[np.ndarray],
+                 max_norm: float, noise_factor: float, noise: Optional[Dict[str, np.ndarray]] = None,
+                 norm_type: float = 2.0):
+    """customized_client.py:51-63: delta = p - last (parameters only); clip_grad_norm_(delta); p = last + delta;
+    upload = state_dict + torch.normal(0, sigma) (numpy add: fp32 + fp32 -> fp32, int64 + fp32 -> fp64).
+
+    ``noise`` (name -> fp32 array of the entry's shape) replaces the reference's torch.normal draws so the
+    device's own stream can be checked; None with noise_factor == 0 means +0.0 noise.
+    Returns (recovered state, upload, total_norm)."""
+    names = list(state.keys())
+    pidx = [i for i, f in enumerate(is_param) if f]
+    deltas = [np.asarray(state[names[i]], np.float32) - np.asarray(l, np.float32) for i, l in zip(pidx, last)]
+    total, coef, apply = dp_clip_coef(deltas, max_norm, norm_type)
+    if apply:
+        deltas = [d * coef for d in deltas]
+    rec = OrderedDict((n, np.array(state[n])) for n in names)
+    for i, l, d in zip(pidx, last, deltas):
+        rec[names[i]] = np.asarray(l, np.float32) + d
+    sigma = noise_factor * max_norm
+    upload = OrderedDict()
+    for n in names:
+        z = (noise[n] if noise is not None else
+             np.zeros(np.shape(rec[n]), np.float32) if sigma == 0 else None)
+        if z is None:
+            raise ValueError("dp_privatize: sigma > 0 needs the noise draws")
+        upload[n] = np.asarray(rec[n] + np.asarray(z, np.float32))
+    return rec, upload, total

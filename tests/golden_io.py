@@ -18,8 +18,12 @@ DEFAULT_ARGS = dict(gradient_policy=None, learning_rate=0.05, min_learning_rate=
 
 
 def scenario_names(kind="single"):
-    """kind 'single': one global model per scenario; 'cohorts': Auxo multi-cohort scenarios."""
+    """kind 'single': one global model per scenario; 'cohorts': Auxo multi-cohort scenarios; 'heterofl';
+    'client': FedProx / local-DP client-side fixtures."""
     names = sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "*.json")))
+    if kind == "client":  # client-side handler fixtures (gen_golden_client.py)
+        return [n for n in names if n.startswith("client_")]
+    names = [n for n in names if not n.startswith("client_")]
     coh = [n for n in names if n.startswith("auxo_")]
     het = [n for n in names if n.startswith("heterofl_")]
     if kind == "cohorts":
@@ -144,3 +148,17 @@ def assert_state_close(got, want, rtol, ctx="", int_slack=0):
         err = np.abs(g.astype(np.float64) - wd)
         bad = err > rtol * scale
         assert not bad.any(), f"{ctx} tensor {i}: {bad.sum()} elements beyond rtol={rtol}, max rel {np.max(err / np.maximum(scale, 1e-30)):.3g}"
+
+
+class ClientScenario:
+    """A client-side fixture (tests/golden/gen_golden_client.py): FedProx steps or one local-DP upload."""
+
+    def __init__(self, name):
+        self.name = name
+        with open(os.path.join(GOLDEN, name + ".json")) as f:
+            self.meta = json.load(f)
+        z = np.load(os.path.join(GOLDEN, name + ".npz"))
+        self.arrays = {k: z[k] for k in z.files}
+
+    def list(self, prefix, n):
+        return [self.arrays[f"{prefix}/{i}"] for i in range(n)]

@@ -1,4 +1,4 @@
-"""CPU-only checks: the C ABI library loads and exports every symbol of include/fedagg.h, the host-side
+"""CPU-only checks: the C ABI library loads and exports every symbol of include/*.h, the host-side
 layout / packing / sharding logic, the host twin of the synthetic generator, and that the product
 package never reaches into oracle/."""
 import ctypes
@@ -13,9 +13,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _header_functions():
-    src = open(os.path.join(ROOT, "include", "fedagg.h")).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(fa_[a-z0-9_]+)\s*\(", src)))
+    names = set()
+    for h in ("fedagg.h", "fedclient.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b(fa_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
 
 
 def test_library_exports_every_declared_symbol():
@@ -23,10 +26,10 @@ def test_library_exports_every_declared_symbol():
 
     lib = ctypes.CDLL(_native.LIB_PATH)
     names = _header_functions()
-    assert len(names) >= 16
+    assert len(names) >= 22
     for n in names:
-        assert hasattr(lib, n), f"{n} declared in include/fedagg.h but not exported"
-    assert sorted(_native.SIGNATURES) == names, "ctypes binding out of sync with include/fedagg.h"
+        assert hasattr(lib, n), f"{n} declared in include/*.h but not exported"
+    assert sorted(_native.SIGNATURES) == names, "ctypes binding out of sync with include/*.h"
     _native.load()  # types every entry point, checks the ABI version (no GPU call)
     assert _native.load().fa_abi_version() == _native.ABI_VERSION
 

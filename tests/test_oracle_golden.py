@@ -58,3 +58,43 @@ def test_oracle_matches_heterofl_fixture(name):
     sd = OrderedDict(zip(sc.names, sc.init_state()))
     heterofl_combine(sd, sc.hetero_locals())
     assert_state_equal(list(sd.values()), sc.expected(0), name)
+
+
+# ---- client-side handlers: oracle vs the real reference's outputs ----------------
+from collections import OrderedDict  # noqa: E402
+
+import numpy as np  # noqa: E402
+
+from tests.golden_io import ClientScenario  # noqa: E402
+
+
+@pytest.mark.parametrize("name", [n for n in scenario_names("client") if "_prox_" in n])
+def test_oracle_fedprox_matches_reference(name):
+    from oracle.cpu_reference import fedprox_update
+
+    sc = ClientScenario(name)
+    T = len(sc.meta["shapes"])
+    glob = sc.list("global", T)
+    for s in range(sc.meta["steps"]):
+        got = fedprox_update(sc.list(f"in/{s}", T), glob, sc.meta["lr"], sc.meta["mu"])
+        for g, w in zip(got, sc.list(f"out/{s}", T)):
+            assert g.dtype == w.dtype and np.array_equal(g, w)
+
+
+@pytest.mark.parametrize("name", [n for n in scenario_names("client") if "_dp_" in n])
+def test_oracle_local_dp_matches_reference(name):
+    from oracle.cpu_reference import dp_privatize
+
+    sc = ClientScenario(name)
+    m = sc.meta
+    names, T = m["names"], len(m["names"])
+    state = OrderedDict(zip(names, sc.list("in", T)))
+    last = sc.list("last", sum(m["is_param"]))
+    noise = dict(zip(names, sc.list("noise", T))) if m["noise_factor"] else None
+    rec, up, total = dp_privatize(state, m["is_param"], last, m["clip"], m["noise_factor"], noise,
+                                  norm_type=m["norm_type"])
+    assert np.float32(total) == np.float32(m["total_norm"])
+    for j, n in enumerate(names):
+        for got, want in ((rec[n], sc.arrays[f"recovered/{j}"]), (up[n], sc.arrays[f"upload/{j}"])):
+            assert got.dtype == want.dtype and got.shape == want.shape, n
+            assert np.array_equal(got, want), n
