@@ -62,7 +62,8 @@ SIGNATURES = {
                                _c_void_p]),
     "fa_dp_apply": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _f32,
                            ctypes.c_uint64, _i32, _c_void_p]),
-    "fa_dp_noise_i64": (_i32, [_c_void_p, _c_void_p, _i64, _f32, ctypes.c_uint64, _i64, _c_void_p]),
+    "fa_dp_noise_i64": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _f32, ctypes.c_uint64,
+                               _c_void_p]),
     "fa_dp_normals": (_i32, [_c_void_p, _i64, ctypes.c_uint64, _i64, _c_void_p]),
 }
 

@@ -23,6 +23,7 @@ distribution, a different stream than torch's CPU generator.
 from __future__ import annotations
 
 import math
+import weakref
 from typing import Dict, Iterable, List, Optional, Union
 
 import numpy as np
@@ -56,13 +57,19 @@ def clip_grad_norm_(parameters: Union[torch.Tensor, Iterable[torch.Tensor]], max
 
 
 class _UploadLayout:
-    """state_dict entries of a model, split into fp32 (packed into one device bucket) and int64 ones."""
+    """state_dict entries of a model, split into fp32 (packed into one device bucket) and int64 ones.
+    Entry i is ``model.parameters()[param_index[i]]`` or ``model.buffers()[buffer_index[i]]``."""
 
     def __init__(self, model: torch.nn.Module):
         sd = model.state_dict(keep_vars=True)
         self.names = list(sd.keys())
         pids = {id(p): i for i, p in enumerate(model.parameters())}
+        bids = {id(b): i for i, b in enumerate(model.buffers())}
         self.param_index = [pids.get(id(sd[n])) for n in self.names]  # position in model.parameters()
+        self.buffer_index = [bids.get(id(sd[n])) for n in self.names]
+        for n, pi, bi in zip(self.names, self.param_index, self.buffer_index):
+            if pi is None and bi is None:
+                raise NotImplementedError(f"{n}: state_dict entry is neither a parameter nor a buffer")
         self.shapes = [tuple(sd[n].shape) for n in self.names]
         self.dtypes = [sd[n].dtype for n in self.names]
         for n, d in zip(self.names, self.dtypes):
@@ -80,15 +87,29 @@ class _UploadLayout:
         self.f_off, self.f_total = offs, o
 
 
+_LAYOUTS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+
+
+def _layout_of(model: torch.nn.Module):
+    """The model's upload layout, rebuilt only when its parameter / buffer objects or shapes change."""
+    params, bufs = list(model.parameters()), list(model.buffers())
+    key = (tuple(map(id, params)), tuple(map(id, bufs)), tuple(p.shape for p in params),
+           tuple(b.shape for b in bufs))
+    ent = _LAYOUTS.get(model)
+    if ent is None or ent[0] != key:
+        ent = (key, _UploadLayout(model))
+        _LAYOUTS[model] = ent
+    return ent[1], params, bufs
+
+
 def privatize_update(model: torch.nn.Module, last_model_params: List[torch.Tensor], clip_threshold: float,
                      noise_factor: float, seed: int = 0, as_numpy: bool = True):
     """customized_client.py:51-63 on the device; returns ``model_param`` ({name: array}) like the reference."""
-    L = _UploadLayout(model)
-    sd = model.state_dict()
-    params = [p.data for p in model.parameters()]
+    L, params, bufs = _layout_of(model)
+    entry = [params[pi] if pi is not None else bufs[bi] for pi, bi in zip(L.param_index, L.buffer_index)]
     if len(last_model_params) != len(params):
         raise ValueError(f"{len(last_model_params)} last-model tensors for {len(params)} parameters")
-    dev = params[0].device if params else next(iter(sd.values())).device
+    dev = entry[0].device
     last = [t.to(dev) if t.device != dev else t for t in last_model_params]
     coef = torch.empty(3, dtype=torch.float32, device=dev)
     if params:
@@ -102,19 +123,17 @@ def privatize_update(model: torch.nn.Module, last_model_params: List[torch.Tenso
     bucket = torch.empty(max(1, L.f_total), dtype=torch.float32, device=dev)
     src, lst, up, offs = [], [], [], []
     for i, o in zip(L.f_idx, L.f_off):
-        t = sd[L.names[i]]
         pi = L.param_index[i]
-        src.append(params[pi] if pi is not None else t)
+        src.append(entry[i])
         lst.append(last[pi] if pi is not None else None)
         up.append(bucket[o:o + L.numel[i]])
         offs.append(L.noise_off[i])
     kx.dp_apply(src, lst, up, offs, coef, sigma, seed, write_param=True)
-    side = {}
-    for i, d in enumerate(L.dtypes):
-        if d == torch.int64:
-            out = torch.empty(L.numel[i], dtype=torch.float64, device=dev)
-            kx.dp_noise_i64(sd[L.names[i]].reshape(-1).contiguous(), out, sigma, seed, L.noise_off[i])
-            side[i] = out
+    side = {i: torch.empty(L.numel[i], dtype=torch.float64, device=dev)
+            for i, d in enumerate(L.dtypes) if d == torch.int64}
+    if side:
+        kx.dp_noise_i64([entry[i].reshape(-1) for i in side], list(side.values()),
+                        [L.noise_off[i] for i in side], sigma, seed)
     if not as_numpy:
         res = {}
         for i, o in zip(L.f_idx, L.f_off):

@@ -22,9 +22,10 @@ class ClientOptimizer(object):
 
     def update_client_weight(self, conf, model, global_model=None):
         if conf.gradient_policy == 'fed-prox':
-            params = [p.data for p in model.parameters()]
+            # the parameters themselves (not .data views: same storage, no per-step tensor objects); the
+            # kernel writes in place outside autograd, like the reference's param.data update
+            params = list(model.parameters())
             if global_model is None or len(global_model) != len(params):
                 raise ValueError("fed-prox needs global_model: one tensor per model parameter")
             # the Python double lr*mu multiplies fp32 tensors, so torch rounds it to fp32 first
-            kx.prox_update(params, [g.data if hasattr(g, "data") else g for g in global_model],
-                           float(conf.learning_rate * conf.proxy_mu))
+            kx.prox_update(params, global_model, float(conf.learning_rate * conf.proxy_mu))

@@ -47,7 +47,7 @@ int check_launch(const char* what) {
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
-constexpr int MT_MAX = 48;               // tensors per launch (kernel-argument table, < 4 KiB)
+constexpr int MT_MAX = 64;               // tensors per launch (kernel-argument table 2.8 KiB, < 4 KiB; `vec` is 64 bits)
 constexpr int MT_THREADS = 256;
 constexpr int MT_UNROLL = 4;             // float4 per thread per chunk
 constexpr int64_t MT_CHUNK = MT_THREADS * 4 * MT_UNROLL;  // 4096 elements per workgroup
@@ -190,38 +190,37 @@ __global__ __launch_bounds__(MT_THREADS) void k_dp_partial(MtList L, double* __r
   }
 }
 
-// pass 2 (one workgroup per launch group): per-tensor total over its workgroups, in workgroup order
+// pass 2 (one wave per tensor): the tensor's total over its workgroup partials.  Lane l sums partials
+// l, l+64, ... in order, then a fixed butterfly combines the lanes: deterministic for a given model.
 template <bool INF>
 __global__ __launch_bounds__(64) void k_dp_tensor_norm(MtList L, const double* __restrict__ part,
                                                       double* __restrict__ tsum) {
-  for (int t = threadIdx.x; t < L.T; t += 64) {
-    double s = 0.0;
-    for (int b = L.blk0[t]; b < L.blk0[t + 1]; ++b) s = INF ? nanmax(s, part[L.part0 + b]) : s + part[L.part0 + b];
-    tsum[L.t0 + t] = s;
-  }
+  const int t = blockIdx.x;
+  double s = 0.0;
+  for (int b = L.blk0[t] + threadIdx.x; b < L.blk0[t + 1]; b += 64)
+    s = INF ? nanmax(s, part[L.part0 + b]) : s + part[L.part0 + b];
+  s = INF ? wave_max(s) : wave_sum(s);
+  if (threadIdx.x == 0) tsum[L.t0 + t] = s;
 }
 
-// pass 3 (one thread): clip_norm.py:36-52 on the per-tensor totals
+// pass 3 (one wave): clip_norm.py:36-52 on the per-tensor totals
 //   norms[t] = fp32 torch.norm(p_t);  total = torch.norm(torch.stack(norms))  (or max for inf)
 //   clip_coef = max_norm / (total + 1e-6)  (fp32);  apply = clip_coef < 1
 template <bool INF>
-__global__ void k_dp_coef(const double* __restrict__ tsum, int T, float max_norm, float* __restrict__ out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  float total;
-  if (T == 0) {
-    total = 0.f;  // clip_norm.py:35-36 returns tensor(0.) and clips nothing
-  } else if (INF) {
-    double m = 0.0;
-    for (int t = 0; t < T; ++t) m = nanmax(m, tsum[t]);
-    total = (float)m;
-  } else {
-    double s = 0.0;
-    for (int t = 0; t < T; ++t) {
+__global__ __launch_bounds__(64) void k_dp_coef(const double* __restrict__ tsum, int T, float max_norm,
+                                               float* __restrict__ out) {
+  double s = 0.0;
+  for (int t = threadIdx.x; t < T; t += 64) {
+    if (INF) {
+      s = nanmax(s, tsum[t]);
+    } else {
       const float nt = (float)sqrt(tsum[t]);  // torch.norm(p, 2) -> fp32 0-d tensor
       s += (double)nt * (double)nt;
     }
-    total = (float)sqrt(s);
   }
+  s = INF ? wave_max(s) : wave_sum(s);
+  if (threadIdx.x != 0) return;
+  const float total = T == 0 ? 0.f : (INF ? (float)s : (float)sqrt(s));  // T == 0: clip_norm.py:35-36
   const float coef = max_norm / (total + 1e-6f);
   out[0] = total;
   out[1] = coef;
@@ -294,10 +293,16 @@ __global__ __launch_bounds__(MT_THREADS) void k_dp_apply(MtList L, const float* 
 }
 
 // int64 state_dict entries (BatchNorm num_batches_tracked): numpy int64 + float32 noise -> float64
-__global__ void k_dp_noise_i64(const int64_t* __restrict__ x, double* __restrict__ out, int64_t n, float sigma,
-                               uint64_t seed, int64_t noff) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-    out[i] = (double)x[i] + (double)noise_at(seed, (uint64_t)(noff + i), sigma);
+// int64 state_dict entries (BatchNorm num_batches_tracked): numpy int64 + float32 noise -> float64.
+// Multi-tensor like the fp32 kernels: a[t] holds the int64 source, c[t] the float64 destination.
+__global__ __launch_bounds__(MT_THREADS) void k_dp_noise_i64(MtList L, float sigma, uint64_t seed) {
+  const int t = find_tensor(L, blockIdx.x);
+  const int64_t n = L.n[t];
+  const int64_t e0 = (int64_t)(blockIdx.x - L.blk0[t]) * MT_CHUNK;
+  const int64_t* __restrict__ x = (const int64_t*)L.a[t];
+  double* __restrict__ out = (double*)L.c[t];
+  for (int64_t i = e0 + threadIdx.x; i < n && i < e0 + MT_CHUNK; i += MT_THREADS)
+    out[i] = (double)x[i] + (double)noise_at(seed, (uint64_t)(L.noff[t] + i), sigma);
 }
 
 // ---- host side: cut the tensor list into launch groups -----------------------------------------
@@ -397,8 +402,8 @@ extern "C" int fa_dp_clip_coef(const float* const* param, const float* const* la
       else hipLaunchKernelGGL(k_dp_partial<false>, dim3(grid), dim3(MT_THREADS), 0, s, L, part);
       if ((rc = check_launch("fa_dp_clip_coef"))) return rc;
     }
-    if (norm_inf) hipLaunchKernelGGL(k_dp_tensor_norm<true>, dim3(1), dim3(64), 0, s, L, part, tsum);
-    else hipLaunchKernelGGL(k_dp_tensor_norm<false>, dim3(1), dim3(64), 0, s, L, part, tsum);
+    if (norm_inf) hipLaunchKernelGGL(k_dp_tensor_norm<true>, dim3(L.T), dim3(64), 0, s, L, part, tsum);
+    else hipLaunchKernelGGL(k_dp_tensor_norm<false>, dim3(L.T), dim3(64), 0, s, L, part, tsum);
     if ((rc = check_launch("fa_dp_clip_coef"))) return rc;
     part0 += grid;
   }
@@ -434,15 +439,28 @@ extern "C" int fa_dp_apply(float* const* param, const float* const* last, float*
   return FA_OK;
 }
 
-extern "C" int fa_dp_noise_i64(const int64_t* x, double* out, int64_t n, float sigma, uint64_t seed,
-                               int64_t noise_offset, fa_stream_t stream) {
-  if (n < 0 || (n > 0 && (!x || !out))) return fail(FA_E_ARG, "fa_dp_noise_i64: bad args");
-  if (n == 0) return FA_OK;
-  int64_t g = (n + 255) / 256;
-  if (g > 1024) g = 1024;
-  hipLaunchKernelGGL(k_dp_noise_i64, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, x, out, n, sigma, seed,
-                     noise_offset);
-  return check_launch("fa_dp_noise_i64");
+extern "C" int fa_dp_noise_i64(const int64_t* const* x, double* const* out, const int64_t* numel,
+                               const int64_t* noise_offset, int32_t T, float sigma, uint64_t seed,
+                               fa_stream_t stream) {
+  if (T < 0 || (T > 0 && (!x || !out || !numel || !noise_offset))) return fail(FA_E_ARG, "fa_dp_noise_i64: bad args");
+  for (int i = 0; i < T; ++i) {
+    if (numel[i] < 0 || (numel[i] > 0 && (!x[i] || !out[i])))
+      return fail(FA_E_ARG, "fa_dp_noise_i64: tensor %d: bad pointer / size", i);
+    if (((uintptr_t)x[i] & 7u) || ((uintptr_t)out[i] & 7u))
+      return fail(FA_E_ARG, "fa_dp_noise_i64: tensor %d: pointers must be 8-byte aligned", i);
+    if (numel[i] > MT_CHUNK * (int64_t)(INT32_MAX / 4)) return fail(FA_E_RANGE, "fa_dp_noise_i64: tensor %d too large", i);
+  }
+  int32_t t = 0;
+  int rc;
+  while (t < T) {
+    MtList L;
+    const int grid = build_group(L, T, &t, (float* const*)x, nullptr, (float* const*)out, numel, noise_offset, 0);
+    if (grid == 0) continue;
+    L.vec = 0;
+    hipLaunchKernelGGL(k_dp_noise_i64, dim3(grid), dim3(MT_THREADS), 0, (hipStream_t)stream, L, sigma, seed);
+    if ((rc = check_launch("fa_dp_noise_i64"))) return rc;
+  }
+  return FA_OK;
 }
 
 // reference normal stream for host-side tests: z[i] for counter i (host twin in fedscale_amd/synth.py)

@@ -181,31 +181,58 @@ def fill_synthetic(x: torch.Tensor, K: int, P: int, *, seed: int, k0: int = 0, s
 
 
 # ---- client-side handlers (include/fedclient.h): multi-tensor launches over HOST pointer tables -----
-class _Table:
-    """Host arrays of device pointers / element counts for one tensor list (kept alive for the call)."""
+# The reference calls FedProx after EVERY local step (torch_client.py:238-240), so the per-call host cost
+# matters as much as the kernel: a validated pointer table is cached per tensor-list signature (device
+# pointers + sizes), and a repeat call is one ctypes call into the library.
+class _Plan:
+    """Validated host tables (device pointers, element counts) for fixed tensor lists."""
 
     def __init__(self, lists, numel):
         import numpy as np
 
-        self.arrays = []
-        for lst in lists:
-            if lst is None:
-                self.arrays.append(None)
-                continue
-            self.arrays.append(np.asarray([0 if t is None else t.data_ptr() for t in lst], dtype=np.uint64))
+        self.arrays = [None if lst is None else
+                       np.asarray([0 if t is None else t.data_ptr() for t in lst], dtype=np.uint64) for lst in lists]
         self.numel = np.asarray(numel, dtype=np.int64)
+        self.T = len(numel)
 
     def ptr(self, i):
         a = self.arrays[i]
         return None if a is None else a.ctypes.data
 
 
-def _fp32_list(ts, name, device=None, allow_none=False):
+_PLANS: "dict" = {}
+_PLANS_MAX = 32
+
+
+def _sig(*lists):
+    out = []
+    for lst in lists:
+        if lst is None:
+            out.append(None)
+        else:
+            out.append(tuple(0 if t is None else t.data_ptr() for t in lst))
+            out.append(tuple(0 if t is None else t.numel() for t in lst))
+            out.append(tuple(None if t is None else (t.dtype, t.device, t.is_contiguous()) for t in lst))
+    return tuple(out)
+
+
+def _cached_plan(kind, lists, build):
+    key = (kind,) + _sig(*lists)
+    plan = _PLANS.get(key)
+    if plan is None:
+        plan = build()
+        if len(_PLANS) >= _PLANS_MAX:
+            _PLANS.pop(next(iter(_PLANS)))
+        _PLANS[key] = plan
+    return plan
+
+
+def _fp32_list(ts, name, device=None, allow_none=False, dtype=torch.float32, align=4):
     dev = device
     for i, t in enumerate(ts):
         if t is None and allow_none:
             continue
-        _dev(t, torch.float32, f"{name}[{i}]", align=4)
+        _dev(t, dtype, f"{name}[{i}]", align=align)
         if dev is None:
             dev = t.device
         elif t.device != dev:
@@ -215,18 +242,23 @@ def _fp32_list(ts, name, device=None, allow_none=False):
 
 def prox_update(params, global_model, c: float):
     """param[t] += c * (param[t] - global[t]) for every tensor, one multi-tensor launch (fa_prox_update)."""
-    params, global_model = list(params), list(global_model)
-    if len(params) != len(global_model):
-        raise ValueError(f"{len(params)} parameters but {len(global_model)} global tensors")
+    params = params if isinstance(params, list) else list(params)
+    global_model = global_model if isinstance(global_model, list) else list(global_model)
     if not params:
         return
-    dev = _fp32_list(params, "param")
-    _fp32_list(global_model, "global_model", dev)
-    for i, (p, g) in enumerate(zip(params, global_model)):
-        if p.shape != g.shape:
-            raise ValueError(f"param[{i}] shape {tuple(p.shape)} != global_model[{i}] shape {tuple(g.shape)}")
-    tab = _Table([params, global_model], [p.numel() for p in params])
-    call("fa_prox_update", tab.ptr(0), tab.ptr(1), tab.numel.ctypes.data, len(params), float(c),
+
+    def build():
+        if len(params) != len(global_model):
+            raise ValueError(f"{len(params)} parameters but {len(global_model)} global tensors")
+        dev = _fp32_list(params, "param")
+        _fp32_list(global_model, "global_model", dev)
+        for i, (p, g) in enumerate(zip(params, global_model)):
+            if p.shape != g.shape:
+                raise ValueError(f"param[{i}] shape {tuple(p.shape)} != global_model[{i}] shape {tuple(g.shape)}")
+        return _Plan([params, global_model], [p.numel() for p in params])
+
+    plan = _cached_plan("prox", (params, global_model), build)
+    call("fa_prox_update", plan.ptr(0), plan.ptr(1), plan.numel.ctypes.data, plan.T, float(c),
          _stream(params[0]))
 
 
@@ -234,15 +266,22 @@ def dp_clip_coef(params, last, max_norm: float, norm_inf: bool, coef_out: torch.
     """coef_out[0:3] <- (total norm of param - last, clip coefficient, apply flag) (fa_dp_clip_coef)."""
     params = list(params)
     last = list(last) if last is not None else [None] * len(params)
-    dev = _fp32_list(params, "param", coef_out.device)
-    _fp32_list(last, "last", dev, allow_none=True)
+
+    def build():
+        dev = _fp32_list(params, "param", coef_out.device)
+        _fp32_list(last, "last", dev, allow_none=True)
+        for i, (p, l) in enumerate(zip(params, last)):
+            if l is not None and l.numel() != p.numel():
+                raise ValueError(f"last[{i}] has {l.numel()} elements, param has {p.numel()}")
+        plan = _Plan([params, last], [p.numel() for p in params])
+        plan.ws_bytes = N.load().fa_dp_workspace_bytes(plan.numel.ctypes.data, plan.T)
+        return plan
+
+    plan = _cached_plan("dpnorm", (params, last), build)
     _dev(coef_out, torch.float32, "coef_out", 3, align=4)
-    tab = _Table([params, last], [p.numel() for p in params])
-    nbytes = N.load().fa_dp_workspace_bytes(tab.numel.ctypes.data, len(params))
-    ws = torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=dev)
-    call("fa_dp_clip_coef", tab.ptr(0), tab.ptr(1), tab.numel.ctypes.data, len(params), float(max_norm),
+    ws = torch.empty((plan.ws_bytes + 7) // 8, dtype=torch.float64, device=coef_out.device)
+    call("fa_dp_clip_coef", plan.ptr(0), plan.ptr(1), plan.numel.ctypes.data, plan.T, float(max_norm),
          1 if norm_inf else 0, ptr(ws), ptr(coef_out), _stream(coef_out))
-    return ws  # keep alive until the stream has consumed it (caller holds the reference)
 
 
 def dp_apply(params, last, upload, noise_offset, coef: torch.Tensor, sigma: float, seed: int,
@@ -253,27 +292,52 @@ def dp_apply(params, last, upload, noise_offset, coef: torch.Tensor, sigma: floa
     params = list(params)
     T = len(params)
     last = list(last) if last is not None else [None] * T
-    dev = _fp32_list(params, "param", coef.device)
-    _fp32_list(last, "last", dev, allow_none=True)
+    upload = None if scale_only else list(upload)
+
+    def build():
+        dev = _fp32_list(params, "param", coef.device)
+        _fp32_list(last, "last", dev, allow_none=True)
+        for i, (p, l) in enumerate(zip(params, last)):
+            if l is not None and l.numel() != p.numel():
+                raise ValueError(f"last[{i}] has {l.numel()} elements, param has {p.numel()}")
+        if upload is not None:
+            _fp32_list(upload, "upload", dev)
+            for i, (p, u) in enumerate(zip(params, upload)):
+                if u.numel() != p.numel():
+                    raise ValueError(f"upload[{i}] has {u.numel()} elements, param has {p.numel()}")
+        plan = _Plan([params, last, upload], [p.numel() for p in params])
+        plan.offs = np.asarray(noise_offset if noise_offset is not None else [0] * T, dtype=np.int64)
+        return plan
+
+    plan = _cached_plan(("dpapply", None if noise_offset is None else tuple(noise_offset)),
+                        (params, last, upload), build)
     _dev(coef, torch.float32, "coef", 3, align=4)
-    if not scale_only:
-        upload = list(upload)
-        _fp32_list(upload, "upload", dev)
-        for i, (p, u) in enumerate(zip(params, upload)):
-            if u.numel() != p.numel():
-                raise ValueError(f"upload[{i}] has {u.numel()} elements, param has {p.numel()}")
-    tab = _Table([params, last, None if scale_only else upload], [p.numel() for p in params])
-    offs = np.asarray(noise_offset if noise_offset is not None else [0] * T, dtype=np.int64)
     flags = (N.FA_DP_WRITE_PARAM if write_param else 0) | (N.FA_DP_SCALE_ONLY if scale_only else 0)
-    call("fa_dp_apply", tab.ptr(0), tab.ptr(1), tab.ptr(2), tab.numel.ctypes.data, offs.ctypes.data, T, ptr(coef),
-         float(sigma), int(seed) & 0xFFFFFFFFFFFFFFFF, flags, _stream(coef))
+    call("fa_dp_apply", plan.ptr(0), plan.ptr(1), plan.ptr(2), plan.numel.ctypes.data, plan.offs.ctypes.data, T,
+         ptr(coef), float(sigma), int(seed) & 0xFFFFFFFFFFFFFFFF, flags, _stream(coef))
 
 
-def dp_noise_i64(x: torch.Tensor, out: torch.Tensor, sigma: float, seed: int, noise_offset: int):
-    _dev(x, torch.int64, "x", align=8)
-    _dev(out, torch.float64, "out", x.numel(), align=8)
-    call("fa_dp_noise_i64", ptr(x), ptr(out), x.numel(), float(sigma), int(seed) & 0xFFFFFFFFFFFFFFFF,
-         int(noise_offset), _stream(x))
+def dp_noise_i64(xs, outs, noise_offset, sigma: float, seed: int):
+    """outs[t] <- float64(xs[t]) + noise, all int64 entries in one launch (fa_dp_noise_i64)."""
+    import numpy as np
+
+    xs, outs = list(xs), list(outs)
+    if not xs:
+        return
+
+    def build():
+        dev = _fp32_list(xs, "x", dtype=torch.int64, align=8)
+        _fp32_list(outs, "out", dev, dtype=torch.float64, align=8)
+        for i, (x, o) in enumerate(zip(xs, outs)):
+            if o.numel() != x.numel():
+                raise ValueError(f"out[{i}] has {o.numel()} elements, x has {x.numel()}")
+        plan = _Plan([xs, outs], [x.numel() for x in xs])
+        plan.offs = np.asarray(noise_offset, dtype=np.int64)
+        return plan
+
+    plan = _cached_plan(("dpi64", tuple(noise_offset)), (xs, outs), build)
+    call("fa_dp_noise_i64", plan.ptr(0), plan.ptr(1), plan.numel.ctypes.data, plan.offs.ctypes.data, plan.T,
+         float(sigma), int(seed) & 0xFFFFFFFFFFFFFFFF, _stream(xs[0]))
 
 
 def dp_normals(out: torch.Tensor, seed: int, noise_offset: int = 0):

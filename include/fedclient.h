@@ -64,9 +64,11 @@ int fa_dp_apply(float* const* param, const float* const* last, float* const* upl
                 const int64_t* noise_offset, int32_t T, const float* coef, float sigma, uint64_t seed, int32_t flags,
                 fa_stream_t stream);
 
-/* int64 state_dict entries: out = double(x) + double(z * sigma)  (numpy int64 + float32 -> float64). */
-int fa_dp_noise_i64(const int64_t* x, double* out, int64_t n, float sigma, uint64_t seed, int64_t noise_offset,
-                    fa_stream_t stream);
+/* int64 state_dict entries (customized_client.py:63 on BatchNorm num_batches_tracked), all T in one launch:
+ *   out[t][i] = double(x[t][i]) + double(z(seed, noise_offset[t] + i) * sigma)
+ * (numpy int64 + float32 -> float64).  Pointers 8-byte aligned. */
+int fa_dp_noise_i64(const int64_t* const* x, double* const* out, const int64_t* numel, const int64_t* noise_offset,
+                    int32_t T, float sigma, uint64_t seed, fa_stream_t stream);
 
 /* The generator alone: out[i] = z(seed, noise_offset + i) (for the distribution tests). */
 int fa_dp_normals(float* out, int64_t n, uint64_t seed, int64_t noise_offset, fa_stream_t stream);

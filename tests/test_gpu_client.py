@@ -212,3 +212,51 @@ def test_dp_sigma_zero_is_exact_recover(gpu_device):
             assert u.dtype == np.float64 and np.array_equal(u, h.astype(np.float64))
         else:
             assert u.dtype == np.float32 and np.array_equal(u, h + np.float32(0))
+
+
+def test_prox_plan_cache_revalidates(gpu_device):
+    """A cached pointer table is reused only for the same pointers, sizes, dtypes and contiguity."""
+    from fedscale_amd import kernels as kx
+
+    a = torch.ones(4, 6, device=gpu_device)
+    g = torch.zeros(4, 6, device=gpu_device)
+    kx.prox_update([a], [g], 0.5)
+    kx.prox_update([a], [g], 0.5)  # cached
+    assert torch.equal(a, torch.full((4, 6), 2.25, device=gpu_device))
+    with pytest.raises(ValueError, match="contiguous"):
+        kx.prox_update([a.t()], [g], 0.5)
+    with pytest.raises(ValueError, match="device tensor"):
+        kx.prox_update([a.cpu()], [g.cpu()], 0.5)
+    with pytest.raises(TypeError, match="dtype"):
+        kx.prox_update([a.double()], [g], 0.5)
+    with pytest.raises(ValueError, match="shape"):
+        kx.prox_update([a], [torch.zeros(24, device=gpu_device)], 0.5)
+
+
+def test_client_optimizer_on_a_real_module(gpu_device):
+    """ClientOptimizer.update_client_weight after real optimizer steps, against the reference formula."""
+    import argparse
+
+    from fedscale_amd.cloud.execution.optimizers import ClientOptimizer
+    from oracle.cpu_reference import fedprox_update
+
+    torch.manual_seed(0)
+    net = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 3), torch.nn.BatchNorm2d(4), torch.nn.Flatten(),
+                              torch.nn.Linear(4 * 6 * 6, 5)).to(gpu_device)
+    glob = [p.data.clone() for p in net.parameters()]
+    sgd = torch.optim.SGD(net.parameters(), lr=0.1)
+    conf = argparse.Namespace(gradient_policy="fed-prox", learning_rate=0.1, proxy_mu=0.5)
+    opt = ClientOptimizer()
+    for _ in range(3):
+        sgd.zero_grad()
+        net(torch.randn(2, 3, 8, 8, device=gpu_device)).square().mean().backward()
+        sgd.step()
+        before = [p.data.cpu().numpy() for p in net.parameters()]
+        opt.update_client_weight(conf, net, glob)
+        want = fedprox_update(before, [g.cpu().numpy() for g in glob], 0.1, 0.5)
+        for p, w in zip(net.parameters(), want):
+            assert np.array_equal(p.data.cpu().numpy(), w)
+    conf.gradient_policy = "fed-avg"  # any other policy: no-op
+    snap = [p.data.clone() for p in net.parameters()]
+    opt.update_client_weight(conf, net, glob)
+    assert all(torch.equal(a, b.data) for a, b in zip(snap, net.parameters()))
