@@ -60,6 +60,25 @@ class DeviceAggregatorMixin:
         opt = self._wrapper().optimizer
         return "qfedavg" if (opt is not None and getattr(opt, "mode", None) == "q-fedavg") else "fedavg"
 
+    def serialize_response(self, responses):
+        """aggregator.py:706-715 (``pickle.dumps``), with the global model's bytes made once per model
+        version: the reference pickles get_weights() again for every executor request
+        (create_client_task :804, get_test_config :816, UPDATE_MODEL :903)."""
+        key = getattr(responses, "egress_key", None)
+        if key is not None:
+            wrappers = self.model_wrapper if isinstance(self.model_wrapper, list) else [self.model_wrapper]
+            for w in wrappers:
+                b = w.egress_bytes(key) if isinstance(w, TorchModelAdapter) else None
+                if b is not None:
+                    return b
+            responses = list(responses)
+        sup = getattr(super(), "serialize_response", None)
+        if sup is not None:
+            return sup(responses)
+        import pickle
+
+        return pickle.dumps(responses)
+
     def update_weight_aggregation(self, results):
         w = self._wrapper()
         if self._is_first_result_in_round() or self._device_round is None:

@@ -17,6 +17,7 @@ Device fast path used by ``DeviceAggregatorMixin``:
 """
 from __future__ import annotations
 
+import itertools
 from typing import List, Optional
 
 import numpy as np
@@ -26,6 +27,19 @@ from ...bucket import BucketLayout, ClientStaging
 from ...round import DeviceRound, default_capacity
 from ...state import FlatState, ShardGroup
 from .model_adapter_base import ModelAdapterBase
+
+
+_EGRESS_IDS = itertools.count(1)
+
+
+class EgressWeights(list):
+    """The list get_weights() returns: a plain list of cloned CPU tensors plus an ``egress_key``.  It
+    pickles as a plain list, so executors unpickle it without this package."""
+
+    egress_key = None
+
+    def __reduce_ex__(self, protocol):
+        return (list, (list(self),))
 
 
 def _resolve_device(device) -> torch.device:
@@ -68,6 +82,8 @@ class TorchModelAdapter(ModelAdapterBase):
         self._s[0].copy_(cur_s.to(torch.int64))
         self._version = 0  # bumps on every device-side model update
         self._host_cache = None
+        self._egress_cache = None
+        self._egress_id = next(_EGRESS_IDS)
         self._module_version = 0 if _load_from is None else -1
 
     # ---- internal buffers ---------------------------------------------------------------------
@@ -126,16 +142,37 @@ class TorchModelAdapter(ModelAdapterBase):
         if self._host_cache is None or self._host_cache[0] != self._version:
             L = self.layout
             full = self.shards.all_gather(self._f[self._cur])
-            f_cpu = torch.empty(L.P_full, dtype=torch.float32, pin_memory=True)
+            # one pinned buffer, reused across versions: every consumer clones out of it
+            f_cpu = self._host_cache[1] if self._host_cache is not None else (
+                torch.empty(L.P_full, dtype=torch.float32, pin_memory=True))
             f_cpu.copy_(full[:L.P_full])
             s_cpu = self._s[self._cur][:L.Q].to("cpu")
             self._host_cache = (self._version, f_cpu, s_cpu)
         return self._host_cache[1], self._host_cache[2]
 
     def get_weights(self) -> List[torch.Tensor]:
-        """torch_model_adapter.py:41-47: cloned CPU tensors in state_dict order (gathers the shards)."""
+        """torch_model_adapter.py:41-47: cloned CPU tensors in state_dict order (gathers the shards).
+
+        The list is tagged with (adapter, model version) so that the aggregator's serialize_response can
+        hand out the pickled bytes of this version, made once per round (``egress_bytes``)."""
         f_cpu, s_cpu = self._host_copy()
-        return [t.clone() for t in self.layout.unpack(f_cpu, s_cpu)]
+        out = EgressWeights(t.clone() for t in self.layout.unpack(f_cpu, s_cpu))
+        out.egress_key = (self._egress_id, self._version)
+        return out
+
+    def egress_bytes(self, key) -> Optional[bytes]:
+        """``pickle.dumps`` of get_weights() for model version ``key`` — the bytes the reference's
+        serialize_response makes per executor request (aggregator.py:788-804, 902-909) — made once per
+        model version from the adapter's own host copy.  None when ``key`` is not the current version."""
+        import pickle
+
+        if key != (self._egress_id, self._version):
+            return None
+        if self._egress_cache is None or self._egress_cache[0] != key:
+            f_cpu, s_cpu = self._host_copy()
+            self._egress_cache = None
+            self._egress_cache = (key, pickle.dumps([t.clone() for t in self.layout.unpack(f_cpu, s_cpu)]))
+        return self._egress_cache[1]
 
     def get_model(self):
         if self._module_version != self._version:

@@ -26,6 +26,7 @@ def main():
     allout = [run(K, rounds, which, w) for w in worker_list]
     # full ingress from the executor's pickled payload (aggregator.py:704 deserialize_response)
     allout.append(run(K, rounds, which, None, loader="pickle"))
+    allout.append(egress(which))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(allout, open(os.path.join(ROOT, "gpurun_out", f"ingress_{which}_k{K}.json"), "w"), indent=1)
 
@@ -90,6 +91,47 @@ def run(K, rounds, which, workers, loader=None):
            "ingress_GBps": 4 * K * P / t_round / 1e9,
            "staging_capacity": adapter.staging.capacity, "pack_workers": adapter.staging.pack_workers,
            "from_payload": loader, "loads_ms_per_update": (t_load * 1e3 if loader else None)}
+    print(json.dumps(out), flush=True)
+    return out
+
+
+def egress(which, requests=8):
+    """Egress per executor request (aggregator.py:788-804, 902-909): get_weights() + serialize_response.
+    The reference pickles the weights again for every request; the mixin serves the bytes made once per
+    model version."""
+    import pickle
+
+    from fedscale_amd import synth
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    names, shapes, dtypes = synth.resnet18_layout() if which == "resnet18" else synth.femnist_cnn_layout()
+    model = synth.LayoutModule(names, shapes, dtypes)
+    adapter = TorchModelAdapter(model, device="cuda:0")
+    agg = DeviceAggregator(adapter)
+    rng = np.random.default_rng(1)
+    upd = {n: (t.numpy() + np.float32(0.01) * rng.standard_normal(t.shape, dtype=np.float32)) if t.dtype != torch.int64
+           else t.numpy() for n, t in model.state_dict().items()}
+    times = {"cached": [], "reference": []}
+    for r in range(3):
+        agg.start_round(2)
+        agg.on_result({"client_id": 0, "update_weight": upd, "moving_loss": 1.0})
+        agg.on_result({"client_id": 1, "update_weight": upd, "moving_loss": 1.0})
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(requests):
+            agg.serialize_response(adapter.get_weights())
+        t1 = time.perf_counter()
+        for _ in range(requests):
+            pickle.dumps(list(adapter.get_weights()))
+        t2 = time.perf_counter()
+        if r > 0:
+            times["cached"].append((t1 - t0) / requests)
+            times["reference"].append((t2 - t1) / requests)
+    out = {"egress": which, "requests_per_round": requests,
+           "cached_ms_per_request": 1e3 * float(np.median(times["cached"])),
+           "reference_pickle_ms_per_request": 1e3 * float(np.median(times["reference"])),
+           "bytes": len(agg.serialize_response(adapter.get_weights()))}
     print(json.dumps(out), flush=True)
     return out
 
