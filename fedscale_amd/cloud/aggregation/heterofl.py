@@ -32,19 +32,25 @@ def _dims(shape):
 
 class PrefixBoxPlan:
     """Device-side launch plan for one combination: global tensor dims, per-(client, tensor) box
-    descriptors into the concatenated uploads, and the workgroup -> (tensor, first element) chunk list."""
+    descriptors into the concatenated uploads, and the workgroup -> (tensor, first element) chunk list.
+
+    Upload layout (``xs``): client after client, tensor after tensor.  The box of a ROW-mode tensor (global
+    rows of >= ROW_MODE_MIN elements) starts 16-byte aligned and its rows are padded to a multiple of 4
+    elements, so the kernel reads 4 columns per dwordx4 load; ELEMENT-mode boxes are packed densely."""
 
     def __init__(self, global_shapes: Sequence, local_shapes: Sequence[Sequence], device):
         self.device = torch.device(device)
         T, K = len(global_shapes), len(local_shapes)
         tens = np.zeros((T, 4), dtype=np.int64)
         goff = 0
+        row_mode = []
         for k, gs in enumerate(global_shapes):
             O, I, S = _dims(gs)
             tens[k] = (goff, O, I, S)
             goff += O * I * S
-        desc = np.zeros((K, T, 3), dtype=np.int64)
-        off = 0
+            row_mode.append(I * S >= ROW_MODE_MIN)
+        desc = np.zeros((K, T, 4), dtype=np.int64)
+        off = data = 0
         for m, shapes in enumerate(local_shapes):
             for k, (ls, gs) in enumerate(zip(shapes, global_shapes)):
                 ls, gs = tuple(ls), tuple(gs)
@@ -52,12 +58,19 @@ class PrefixBoxPlan:
                 o, i, _ = _dims(ls)
                 if len(ls) != len(gs) or ls[2:] != gs[2:] or o > O or i > I:
                     raise ValueError(f"client {m} tensor {k}: shape {ls} is not a prefix box of {gs}")
-                desc[m, k] = (off, o, i * S)  # box rows are i*S long in the upload
-                off += o * i * S
+                L = i * S
+                if row_mode[k]:
+                    off = (off + 3) // 4 * 4
+                    ld = (L + 3) // 4 * 4
+                else:
+                    ld = L
+                desc[m, k] = (off, o, L, ld)
+                off += o * ld
+                data += o * L
         ck_t, ck_f = [], []  # ck_t holds (tensor, row) pairs; row -1 = element mode
         for k in range(T):
             O, RL = int(tens[k, 1]), int(tens[k, 2] * tens[k, 3])
-            if RL >= ROW_MODE_MIN:
+            if row_mode[k]:
                 for o in range(O):
                     for f in range(0, RL, HB_ELEMS):
                         ck_t += [k, o]
@@ -66,7 +79,10 @@ class PrefixBoxPlan:
                 for f in range(0, O * RL, HB_ELEMS):
                     ck_t += [k, -1]
                     ck_f.append(f)
-        self.K, self.T, self.P, self.upload_elems = K, T, goff, off
+        self.K, self.T, self.P = K, T, goff
+        self.upload_elems = (off + 3) // 4 * 4  # xs size including the row padding
+        self.upload_data_elems = data           # the clients' actual parameters
+        self.desc_host = desc
         self.tens_host = tens
         self.d_desc = torch.from_numpy(desc.reshape(-1)).to(self.device)
         self.d_tens = torch.from_numpy(tens.reshape(-1)).to(self.device)
@@ -74,13 +90,25 @@ class PrefixBoxPlan:
         self.d_cf = torch.tensor(ck_f, dtype=torch.int64, device=self.device)
         self.nchunks = len(ck_f)
 
+    def pack(self, m: int, k: int, a: np.ndarray, xv: np.ndarray) -> None:
+        """Copy client m's box of tensor k into the upload buffer xv at its (padded) place."""
+        off, o, L, ld = (int(v) for v in self.desc_host[m, k])
+        if a.size != o * L:
+            raise ValueError(f"client {m} tensor {k}: {a.size} elements, the plan expects {o * L}")
+        if ld == L:
+            xv[off:off + o * L] = a.reshape(-1)
+        else:
+            xv[off:off + o * ld].reshape(o, ld)[:, :L] = a.reshape(o, L)
+
     def run(self, xs: torch.Tensor, glob: torch.Tensor) -> None:
-        """glob (fp32 [P], device) <- HeteroFL combination of the uploads xs (fp32, device, concatenated)."""
+        """glob (fp32 [P], device) <- HeteroFL combination of the uploads xs (fp32, device, plan layout)."""
         if xs.numel() < self.upload_elems or glob.numel() < self.P:
             raise ValueError("PrefixBoxPlan.run: buffers smaller than the plan")
         for t, n in ((xs, "xs"), (glob, "glob")):
             if t.device != self.device or t.dtype != torch.float32 or not t.is_contiguous():
                 raise ValueError(f"PrefixBoxPlan.run: {n} must be a contiguous fp32 tensor on {self.device}")
+        if xs.data_ptr() % 16:
+            raise ValueError("PrefixBoxPlan.run: xs must be 16-byte aligned")
         N.call("fa_prefix_box_combine", xs.data_ptr(), self.d_desc.data_ptr(), self.K, self.d_tens.data_ptr(),
                self.T, self.d_ct.data_ptr(), self.d_cf.data_ptr(), self.nchunks, glob.data_ptr(),
                torch.cuda.current_stream(self.device).cuda_stream)
@@ -99,17 +127,15 @@ def combine_prefix_boxes(global_state, local_states: Sequence, device=None) -> N
                                       f"(got {global_state[n].dtype})")
     plan = PrefixBoxPlan([tuple(global_state[n].shape) for n in names],
                          [[tuple(loc[n].shape) for n in names] for loc in local_states], dev)
-    xs_host = torch.empty(max(plan.upload_elems, 1), dtype=torch.float32, pin_memory=True)
+    xs_host = torch.zeros(max(plan.upload_elems, 4), dtype=torch.float32, pin_memory=True)
     xv = xs_host.numpy()
-    pos = 0
-    for loc in local_states:
-        for n in names:
+    for m, loc in enumerate(local_states):
+        for k, n in enumerate(names):
             a = loc[n]
             a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
             if a.dtype != np.float32:
                 raise TypeError(f"{n}: local dtype {a.dtype}, expected float32")
-            xv[pos:pos + a.size] = a.reshape(-1)
-            pos += a.size
+            plan.pack(m, k, a, xv)
     glob = torch.cat([global_state[n].detach().reshape(-1).cpu() for n in names]).to(dev)
     plan.run(xs_host.to(dev, non_blocking=True), glob)
     out = glob.cpu()

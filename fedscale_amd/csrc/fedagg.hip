@@ -915,18 +915,36 @@ extern "C" int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uin
 // A client at model rate r uploads, for every tensor of shape (O, I, S...), the prefix box
 // [0:o) x [0:i) x S (examples/heterofl/customized_fllibs.py:25-70 only ever builds prefix index sets).
 // Per global element, the reference sums the covering clients' values in client order into an fp32
-// zero, counts them, and replaces the element by sum / count where count > 0.  One thread per element;
-// a workgroup covers HB_ELEMS elements of ONE tensor, so the per-client box descriptors are uniform
-// (scalar loads) and a client's covered elements are contiguous runs of its upload.
+// zero, counts them, and replaces the element by sum / count where count > 0.
+//
+// desc[(m*T + k)*4 + {0,1,2,3}] = {offset of client m's box of tensor k in xs, o_m, L_m = i_m*S, ld_m}:
+// the box is o_m rows of L_m elements at row stride ld_m.  A chunk is (tensor k, row o, first column r0)
+// in ROW mode: o is uniform, so "client m covers this row" is a scalar branch; the host pads every box
+// row to ld_m = round_up(L_m, 4) with a 16-byte aligned offset, so each thread takes 4 consecutive
+// columns with ONE dwordx4 load per client (the padding is read, never counted).  ELEMENT mode (k, -1,
+// first element) serves tensors with short rows (1-D BatchNorm vectors ...) one element per thread.
 #define HB_ELEMS 1024
 #ifndef HB_U
 #define HB_U 8
 #endif  // HB_U: clients whose loads are issued before their (in-order) adds
+#ifndef HB_NT
+#define HB_NT 0
+#endif  // HB_NT: non-temporal box loads (every upload element is read exactly once)
+__device__ __forceinline__ f4 hb_load(const float* p) {
+#if HB_NT
+  return __builtin_nontemporal_load((const f4*)p);
+#else
+  return *(const f4*)p;
+#endif
+}
 
-// desc[(m*T + k)*3 + {0,1,2}] = {offset of client m's box of tensor k in xs, o_m, L_m = i_m*S}
-// (host-precomputed row length).  A chunk is (tensor k, row o >= 0, first column r0) in ROW mode, where
-// o is uniform so "client m covers this row" is a scalar branch and the covered columns are the prefix
-// r < L_m of the row; or (k, -1, first element) in ELEMENT mode for tensors with short rows (1-D ...).
+__device__ __forceinline__ void hb_add(float& acc, int& cnt, float v, bool hit) {
+  if (hit) {
+    acc = acc + v;  // tmp_v[idx] += local_parameters[k], clients in order
+    ++cnt;          // count[k][idx] += 1
+  }
+}
+
 __global__ __launch_bounds__(256) void k_prefix_box(const float* __restrict__ xs, const int64_t* __restrict__ desc,
                                                     int K, int T, const int64_t* __restrict__ tens,
                                                     const int32_t* __restrict__ ck_t,
@@ -936,22 +954,55 @@ __global__ __launch_bounds__(256) void k_prefix_box(const float* __restrict__ xs
   const int row = ck_t[2 * c + 1];
   const int64_t goff = tens[4 * k];
   const int64_t RL = tens[4 * k + 2] * tens[4 * k + 3];  // global row length I*S
-  const int64_t n = tens[4 * k + 1] * RL;
-  const int64_t* dk = desc + 3 * (int64_t)k;
-  const int64_t dstride = 3 * (int64_t)T;
-  for (int j = 0; j < HB_ELEMS / 256; ++j) {
-    int64_t o, r;
-    if (row >= 0) {
-      o = row;
-      r = ck_first[c] + j * 256 + threadIdx.x;
-      if (r >= RL) break;
-    } else {
-      const int64_t e = ck_first[c] + j * 256 + threadIdx.x;
-      if (e >= n) break;
-      o = e / RL;
-      r = e - o * RL;
+  const int64_t* dk = desc + 4 * (int64_t)k;
+  const int64_t dstride = 4 * (int64_t)T;
+  if (row >= 0) {
+    const int64_t o = row;
+    const int64_t r = ck_first[c] + 4 * (int64_t)threadIdx.x;  // 4 columns per thread, 16-byte aligned
+    if (r >= RL) return;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};  // tmp_v = v.new_zeros(..., dtype=torch.float32)
+    int cnt[4] = {0, 0, 0, 0};
+    int m = 0;
+    for (; m + HB_U <= K; m += HB_U) {
+      f4 t[HB_U];
+      int64_t len[HB_U];
+#pragma unroll
+      for (int u = 0; u < HB_U; ++u) {
+        const int64_t* d = dk + (int64_t)(m + u) * dstride;
+        len[u] = o < d[1] ? d[2] : 0;  // row covered (scalar) -> its covered columns are [0, L_m)
+        t[u] = r < len[u] ? hb_load(xs + d[0] + o * d[3] + r) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int u = 0; u < HB_U; ++u) {
+        hb_add(acc[0], cnt[0], t[u].x, r < len[u]);
+        hb_add(acc[1], cnt[1], t[u].y, r + 1 < len[u]);
+        hb_add(acc[2], cnt[2], t[u].z, r + 2 < len[u]);
+        hb_add(acc[3], cnt[3], t[u].w, r + 3 < len[u]);
+      }
     }
-    float acc = 0.f;  // tmp_v = v.new_zeros(..., dtype=torch.float32)
+    for (; m < K; ++m) {
+      const int64_t* d = dk + (int64_t)m * dstride;
+      const int64_t len = o < d[1] ? d[2] : 0;
+      if (r < len) {
+        const f4 v = hb_load(xs + d[0] + o * d[3] + r);
+        hb_add(acc[0], cnt[0], v.x, true);
+        hb_add(acc[1], cnt[1], v.y, r + 1 < len);
+        hb_add(acc[2], cnt[2], v.z, r + 2 < len);
+        hb_add(acc[3], cnt[3], v.w, r + 3 < len);
+      }
+    }
+    float* g = glob + goff + o * RL + r;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (r + j < RL && cnt[j] > 0) g[j] = __fdiv_rn(acc[j], (float)cnt[j]);  // tmp_v[count>0].div_(count[..])
+    return;
+  }
+  const int64_t n = tens[4 * k + 1] * RL;
+  for (int j = 0; j < HB_ELEMS / 256; ++j) {
+    const int64_t e = ck_first[c] + j * 256 + threadIdx.x;
+    if (e >= n) break;
+    const int64_t o = e / RL, r = e - o * RL;
+    float acc = 0.f;
     int cnt = 0;
     int m = 0;
     for (; m + HB_U <= K; m += HB_U) {
@@ -961,23 +1012,16 @@ __global__ __launch_bounds__(256) void k_prefix_box(const float* __restrict__ xs
       for (int u = 0; u < HB_U; ++u) {
         const int64_t* d = dk + (int64_t)(m + u) * dstride;
         hit[u] = o < d[1] && r < d[2];
-        t[u] = hit[u] ? xs[d[0] + o * d[2] + r] : 0.f;
+        t[u] = hit[u] ? xs[d[0] + o * d[3] + r] : 0.f;
       }
 #pragma unroll
-      for (int u = 0; u < HB_U; ++u)
-        if (hit[u]) {
-          acc = acc + t[u];  // tmp_v[idx] += local_parameters[k], clients in order
-          ++cnt;             // count[k][idx] += 1
-        }
+      for (int u = 0; u < HB_U; ++u) hb_add(acc, cnt, t[u], hit[u]);
     }
     for (; m < K; ++m) {
       const int64_t* d = dk + (int64_t)m * dstride;
-      if (o < d[1] && r < d[2]) {
-        acc = acc + xs[d[0] + o * d[2] + r];
-        ++cnt;
-      }
+      if (o < d[1] && r < d[2]) hb_add(acc, cnt, xs[d[0] + o * d[3] + r], true);
     }
-    if (cnt > 0) glob[goff + o * RL + r] = __fdiv_rn(acc, (float)cnt);  // tmp_v[count>0].div_(count[..])
+    if (cnt > 0) glob[goff + o * RL + r] = __fdiv_rn(acc, (float)cnt);
   }
 }
 
@@ -988,6 +1032,7 @@ extern "C" int fa_prefix_box_combine(const float* xs, const int64_t* desc, int32
   if (nchunks == 0 || K == 0) return FA_OK;
   if (!xs || !desc || !tensors || !chunk_tensor || !chunk_first || !global)
     return fail(FA_E_ARG, "fa_prefix_box_combine: NULL pointer");
+  if (!aligned16(xs)) return fail(FA_E_ARG, "fa_prefix_box_combine: xs must be 16-byte aligned");
   hipLaunchKernelGGL(k_prefix_box, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, xs, desc, (int)K, (int)T, tensors,
                      chunk_tensor, chunk_first, global);
   return check_launch("fa_prefix_box_combine");

@@ -150,10 +150,14 @@ int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uint32_t seed,
  * HeteroFL sub-model combination: replaces Customized_Aggregator.combine_models,
  * examples/heterofl/customized_aggregator.py:78-119 (index sets from customized_fllibs.py:25-70 are
  * prefixes, so client m's upload of tensor k is the box [0:o) x [0:i) x S of the global (O, I, S)).
- *   xs       concatenated client uploads (fp32), desc[(m*T + k)*3 + {0,1,2}] = {offset in xs, o, i*S}
+ *   xs       concatenated client uploads (fp32, 16-byte aligned),
+ *            desc[(m*T + k)*4 + {0,1,2,3}] = {offset in xs, o, L = i*S, ld}: client m's box of tensor k is
+ *            o rows of L elements at row stride ld.  For ROW-mode tensors the offset must be a multiple
+ *            of 4 and ld = round_up(L, 4) (rows padded to 16 bytes; the padding is read, never counted);
+ *            ELEMENT-mode tensors may use ld = L at any offset.
  *   tensors  [T][4] = {offset in global, O, I, S};  chunk_tensor[2c] = tensor of workgroup c,
- *            chunk_tensor[2c+1] = row o (>= 0: columns [chunk_first[c], +1024) of that row) or -1
- *            (elements [chunk_first[c], +1024) of the flattened tensor)
+ *            chunk_tensor[2c+1] = row o (>= 0: columns [chunk_first[c], +1024) of that row, chunk_first
+ *            a multiple of 4) or -1 (elements [chunk_first[c], +1024) of the flattened tensor)
  * global[e] <- (sum over covering clients, client order, fp32 from 0) / fp32(count) where count > 0.
  */
 int fa_prefix_box_combine(const float* xs, const int64_t* desc, int32_t K, const int64_t* tensors, int32_t T,

@@ -389,3 +389,35 @@ def test_egress_bytes_cached_per_model_version(gpu_device):
     assert_state_equal(got, sc.expected(0), "egress")
     assert all(torch.equal(a, b) for a, b in zip(got, w))
     assert pickle.loads(agg.serialize_response({"x": 1})) == {"x": 1}  # other responses: plain pickle
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_heterofl_random_prefix_boxes_bit_exact(gpu_device, seed):
+    """Random global shapes (row lengths off the 4-grid, conv kernels, 1-D and 0-d-free vectors, rows in
+    both kernel modes) and random per-client prefix boxes, more clients than one load batch, against the
+    oracle restatement of combine_models — bit-exact."""
+    from collections import OrderedDict
+
+    from fedscale_amd.cloud.aggregation.heterofl import combine_prefix_boxes
+    from oracle.cpu_reference import heterofl_combine
+
+    rng = np.random.default_rng(seed)
+    shapes = [(37, 29, 3, 3), (64, 300), (5, 1023), (130,), (7, 2, 5), (258, 257), (3, 1025, 1), (11, 255)]
+    glob = OrderedDict((f"t{i}", torch.from_numpy(rng.normal(0, 1, size=s).astype(np.float32)))
+                       for i, s in enumerate(shapes))
+    K = 19
+    locs = []
+    for m in range(K):
+        loc = OrderedDict()
+        for n, v in glob.items():
+            s = tuple(v.shape)
+            o = int(rng.integers(0, s[0] + 1)) if m % 4 else s[0]
+            box = (o,) + ((int(rng.integers(1, s[1] + 1)),) if len(s) > 1 else ()) + s[2:]
+            loc[n] = rng.normal(0, 1, size=box).astype(np.float32)
+        locs.append(loc)
+    want = OrderedDict((n, v.clone()) for n, v in glob.items())
+    heterofl_combine(want, locs)
+    got = OrderedDict((n, v.clone()) for n, v in glob.items())
+    combine_prefix_boxes(got, locs, device=gpu_device)
+    for n in glob:
+        assert torch.equal(got[n], want[n]), n

@@ -49,8 +49,9 @@ def main():
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
-    alg = 4 * plan.upload_elems + 8 * plan.P  # every upload element read once; global read + written
-    out = {"K": K, "P": plan.P, "upload_elems": plan.upload_elems, "kernel_ms": ms,
+    alg = 4 * plan.upload_data_elems + 8 * plan.P  # every uploaded parameter read once; global read + written
+    out = {"K": K, "P": plan.P, "upload_elems": plan.upload_data_elems, "padded_elems": plan.upload_elems,
+           "kernel_ms": ms,
            "GBps": alg / (ms * 1e-3) / 1e9, "client_updates_per_s": K / (ms * 1e-3)}
     print(json.dumps(out))
     json.dump(out, open(os.path.join(ROOT, "gpurun_out", "heterofl_bench.json"), "w"), indent=1)
