@@ -39,3 +39,22 @@ def test_shards_tile_and_roundtrip(entries, world, seed):
     out = full.unpack(torch.from_numpy(flat), torch.from_numpy(side))
     for o, v in zip(out, vals):
         np.testing.assert_array_equal(o.numpy(), v)
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.integers(1, 5000), st.integers(1, 16))
+def test_client_blocks_partition_arrivals(K, world):
+    """Client mode (state.py): the ranks' arrival blocks are contiguous, in rank order, cover 0..K-1
+    exactly once, differ in size by at most one, and owner() names the block holding each arrival."""
+    from fedscale_amd.state import ShardGroup
+
+    g = ShardGroup(0, world, mode="clients")
+    blocks = [g.client_block(K, r) for r in range(world)]
+    assert blocks[0][0] == 0 and blocks[-1][1] == K
+    assert all(blocks[r][1] == blocks[r + 1][0] for r in range(world - 1))
+    sizes = [b - a for a, b in blocks]
+    assert max(sizes) - min(sizes) <= 1
+    ks = np.unique(np.linspace(0, K - 1, num=min(K, 64)).astype(int))
+    for k in ks:
+        a, b = blocks[g.owner(int(k), K)]
+        assert a <= k < b

@@ -23,7 +23,7 @@ fi
 if [[ $STAGE == all || $STAGE == prof ]]; then
   run rocprof
   export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $ROOT/bench.py --steps 10 --warmup 2 --cpu-seconds 0 > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $ROOT/bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-other-configs > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }
   tail -1 $OUT/prof.log
   find $OUT/prof -name "*kernel_stats.csv" | head -3
 fi
