@@ -928,7 +928,7 @@ extern "C" int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uin
 #define HB_U 8
 #endif  // HB_U: clients whose loads are issued before their (in-order) adds
 #ifndef HB_NT
-#define HB_NT 0
+#define HB_NT 1
 #endif  // HB_NT: non-temporal box loads (every upload element is read exactly once)
 __device__ __forceinline__ f4 hb_load(const float* p) {
 #if HB_NT
