@@ -114,7 +114,8 @@ struct RedArgs {
   const float* x;
   int64_t ld4;  // row stride in float4
   int64_t P4;   // float4 columns to produce (ceil(P/4))
-  int64_t col0; // first float4 column of this launch (a launch covers [col0, min(P4, col0 + grid*span)))
+  int64_t col0; // first float4 column of this launch (a launch covers [col0, min(P4, col0 + ntiles*span)))
+  int64_t ntiles;  // tiles of this launch; workgroup b takes tiles b, b + grid, ...
   int K;
   int flags;
   const float* a;
@@ -133,12 +134,11 @@ struct RedArgs {
 #ifndef FA_RED_WAVES
 #define FA_RED_WAVES 4
 #endif
+// One tile: the workgroup's FA_RED_WAVES waves each own 64*V float4 columns and walk all K clients.
 template <int V, int U, int EPI, bool W>
-__global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int64_t c0 = r.col0 + ((int64_t)blockIdx.x * FA_RED_WAVES + wave) * (64 * V) + lane;
+__device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int lane, int wave) {
   const f4* __restrict__ xp = reinterpret_cast<const f4*>(r.x);
+  const int64_t c0 = r.col0 + (tile * FA_RED_WAVES + wave) * (64 * V) + lane;
 
   bool ok[V];
 #pragma unroll
@@ -220,13 +220,31 @@ __global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
   }
 }
 
+// LOOP = false: workgroup b reduces tile b (grid = tiles).  LOOP = true: a capped grid, workgroup b
+// reduces tiles b, b + grid, ... (r.ntiles in this launch): fewer concurrent column streams per round.
+template <int V, int U, int EPI, bool W, bool LOOP>
+__global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  if (LOOP) {
+    for (int64_t tile = blockIdx.x; tile < r.ntiles; tile += gridDim.x) reduce_tile<V, U, EPI, W>(r, tile, lane, wave);
+  } else {
+    reduce_tile<V, U, EPI, W>(r, blockIdx.x, lane, wave);
+  }
+}
+
 // Launch plan.  Each wave owns a column tile of V KiB (V float4 per lane) and walks all K clients, so a
-// tile is K*V KiB of reads.  Wide tiles keep few DRAM pages open per client row (measured: V=32 reads at
-// the stream-read ceiling, V=2 ~6 % below, profiles/r01_tune_sweep.log); but with few, long tiles the
-// last wave of workgroups leaves CUs idle.  So the columns are cut into up to three launches: the
-// widest variant takes as many FULL waves of workgroups as fit (occupancy x CUs, queried at run time),
-// the next narrower variant the same on what is left, the narrowest the remainder.  Every column is
-// still reduced by exactly one thread in arrival order, so the split never changes a bit.
+// tile is K*V KiB of reads.  Two measured effects shape it (profiles/r01_tune_grid_sweep.log):
+//   * wide tiles keep few DRAM pages open per client row: V=32 reads fastest, V=2 ~6 % slower;
+//   * FEWER concurrent column streams read faster: ~0.75 workgroup of V=32 per CU (192 on 256 CUs),
+//     each walking several tiles, beats one workgroup per CU by 3-4 % (7.08 vs 6.83 TB/s at 1000 x 25M;
+//     6.76 vs 6.56 at 11.19 M; 7.0 vs 6.4 at 6.25 M) — the grid is capped and every workgroup takes the
+//     same number of tiles (grid = ceil(tiles / ceil(tiles / cap))).
+// So a bucket with at least ~0.85 x cap widest tiles is one capped V=32 launch.  Smaller buckets need
+// the parallelism of narrower tiles: the widest variant takes as many FULL waves of workgroups as fit
+// (occupancy x CUs, queried at run time), the next narrower variant the same on what is left, the
+// narrowest the remainder.  Every column is still reduced by exactly one thread in arrival order, so no
+// plan changes a bit of the result.
 #ifdef FA_RED_V  // tuning build: a single fixed variant
 #define FA_LEVELS 1
 #define FA_L0_V FA_RED_V
@@ -242,6 +260,20 @@ __global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
 #define FA_L3_V 2
 #define FA_L3_U 8
 #endif
+#ifndef FA_GRID_CAP_PCT
+#define FA_GRID_CAP_PCT 75  // concurrent V=32 workgroups as a percentage of the CU count
+#endif
+
+static int cu_count() {
+  static int cache[64];  // per device ordinal (idempotent, benign race)
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (cache[dev] > 0) return cache[dev];
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+  cache[dev] = cus;
+  return cus;
+}
 
 template <int V, int U, int EPI, bool W>
 static int resident_blocks() {
@@ -249,21 +281,22 @@ static int resident_blocks() {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
   if (cache[dev] > 0) return cache[dev];
-  int per_cu = 0, cus = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&k_reduce<V, U, EPI, W>),
-                                                   64 * FA_RED_WAVES, 0) != hipSuccess)
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+          &per_cu, reinterpret_cast<const void*>(&k_reduce<V, U, EPI, W, false>), 64 * FA_RED_WAVES, 0) != hipSuccess)
     return 0;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-  cache[dev] = per_cu * cus;
+  cache[dev] = per_cu * cu_count();
   return cache[dev];
 }
 
 // launch variant (V, U) over float4 columns [col, col_end); `full_waves_only` keeps only whole waves of
 // workgroups (a last partial wave is kept when it would still occupy >= 90 % of the resident slots: a
 // narrower variant is ~6 % slower per byte, so handing such a wave down costs more than its idle 10 %)
-// and returns the first column it did not cover.
+// and returns the first column it did not cover.  `cap` > 0: at most `cap` workgroups, each reducing an
+// equal number of tiles (the LOOP kernel).
 template <int V, int U, int EPI, bool W>
-static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_waves_only, hipStream_t st) {
+static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_waves_only, int64_t cap,
+                            hipStream_t st) {
   const int64_t span = 64LL * FA_RED_WAVES * V;
   int64_t nblk = (col_end - col + span - 1) / span;
   if (full_waves_only) {
@@ -275,7 +308,14 @@ static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_w
   }
   if (nblk <= 0) return col;
   r.col0 = col;
-  hipLaunchKernelGGL((k_reduce<V, U, EPI, W>), dim3((unsigned)nblk), dim3(64 * FA_RED_WAVES), 0, st, r);
+  r.ntiles = nblk;
+  if (cap > 0 && nblk > cap) {
+    const int64_t rounds = (nblk + cap - 1) / cap;
+    const int64_t grid = (nblk + rounds - 1) / rounds;
+    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, true>), dim3((unsigned)grid), dim3(64 * FA_RED_WAVES), 0, st, r);
+  } else {
+    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, false>), dim3((unsigned)nblk), dim3(64 * FA_RED_WAVES), 0, st, r);
+  }
   const int64_t end = col + nblk * span;
   return (full_waves_only && end < col_end) ? end : col_end;
 }
@@ -284,15 +324,26 @@ template <int EPI, bool W>
 static void launch_plan(const RedArgs& r, hipStream_t st) {
   int64_t col = 0;
 #if FA_LEVELS == 1
-  launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, false, st);
+#if defined(FA_RED_GRID) && FA_RED_GRID > 0
+  launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, false, FA_RED_GRID, st);  // tuning: fixed cap
 #else
+  launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, false, 0, st);
+#endif
+#else
+  const int64_t cap = (int64_t)cu_count() * FA_GRID_CAP_PCT / 100;
+  const int64_t span0 = 64LL * FA_RED_WAVES * FA_L0_V;
+  const int64_t tiles0 = (r.P4 + span0 - 1) / span0;
+  if (cap > 0 && tiles0 * 20 >= cap * 17) {  // enough widest tiles to keep ~cap workgroups busy
+    launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, 0, r.P4, false, cap, st);
+    return;
+  }
 #ifndef FA_YOGI_SKIP_L0
 #define FA_YOGI_SKIP_L0 0
 #endif
-  if (!(EPI == EPI_YOGI && FA_YOGI_SKIP_L0)) col = launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, true, st);
-  if (col < r.P4) col = launch_level<FA_L1_V, FA_L1_U, EPI, W>(r, col, r.P4, true, st);
-  if (col < r.P4) col = launch_level<FA_L2_V, FA_L2_U, EPI, W>(r, col, r.P4, true, st);
-  if (col < r.P4) launch_level<FA_L3_V, FA_L3_U, EPI, W>(r, col, r.P4, false, st);
+  if (!(EPI == EPI_YOGI && FA_YOGI_SKIP_L0)) col = launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, true, 0, st);
+  if (col < r.P4) col = launch_level<FA_L1_V, FA_L1_U, EPI, W>(r, col, r.P4, true, 0, st);
+  if (col < r.P4) col = launch_level<FA_L2_V, FA_L2_U, EPI, W>(r, col, r.P4, true, 0, st);
+  if (col < r.P4) launch_level<FA_L3_V, FA_L3_U, EPI, W>(r, col, r.P4, false, 0, st);
 #endif
 }
 

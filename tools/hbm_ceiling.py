@@ -20,7 +20,7 @@ def main():
     x = torch.ones(n, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     res = {}
-    for grid in (1024, 2048, 4096, 8192):
+    for grid in (192, 256, 384, 512, 768, 1024, 2048, 4096, 8192):
         out = torch.empty(grid * 256, device="cuda")
         for unroll in (8, 16):
             ts = []
