@@ -29,7 +29,7 @@ if [[ $STAGE == all || $STAGE == prof ]]; then
 fi
 if [[ $STAGE == pmc ]]; then
   export TMPDIR=/tmp
-  ARGS="--steps 3 --warmup 1 --cpu-seconds 0"
+  ARGS="--steps 3 --warmup 1 --cpu-seconds 0 --no-other-configs"
   timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch -o run -- python3 $ROOT/bench.py $ARGS > $OUT/pmc_fetch.log 2>&1 || { tail -20 $OUT/pmc_fetch.log; exit 1; }
   timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write -o run -- python3 $ROOT/bench.py $ARGS > $OUT/pmc_write.log 2>&1 || { tail -20 $OUT/pmc_write.log; exit 1; }
   rm -f profiles/pmc_traffic.json
