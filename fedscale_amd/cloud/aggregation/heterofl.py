@@ -59,6 +59,7 @@ def _global_dims(global_shapes):
     return dims, [I * S >= ROW_MODE_MIN for (_, I, S) in dims]
 
 
+_DTYPES = (torch.float32, torch.int64)  # int64 entries (BatchNorm num_batches_tracked) go through fp32
 _CHUNKS: dict = {}
 
 
@@ -164,8 +165,8 @@ def combine_prefix_boxes(global_state, local_states: Sequence, device=None) -> N
     if not local_states:
         return
     for n in names:
-        if global_state[n].dtype != torch.float32:
-            raise NotImplementedError(f"{n}: HeteroFL combination supports float32 entries "
+        if global_state[n].dtype not in _DTYPES:
+            raise NotImplementedError(f"{n}: HeteroFL combination supports float32 and int64 entries "
                                       f"(got {global_state[n].dtype})")
     st = PrefixBoxStaging([tuple(global_state[n].shape) for n in names], len(local_states), dev)
     for loc in local_states:
@@ -246,8 +247,11 @@ class PrefixBoxStaging:
         for n in names:
             a = local_parameters[n]
             a = a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
-            if a.dtype != np.float32:
-                raise TypeError(f"{n}: local dtype {a.dtype}, expected float32")
+            if a.dtype == np.int64:
+                # the reference's fp32 tmp_v += int64 local converts element-wise (customized_aggregator.py:114)
+                a = a.astype(np.float32)
+            elif a.dtype != np.float32:
+                raise TypeError(f"{n}: local dtype {a.dtype}, expected float32 (or int64)")
             arrays.append(a)
         shapes = [tuple(a.shape) for a in arrays]
         start = (self.off + 63) // 64 * 64  # each client's H2D lands 256-byte aligned
@@ -274,6 +278,7 @@ class PrefixBoxStaging:
         out = glob.cpu()
         for k, n in enumerate(names):
             v = global_state[n]
+            # v[count > 0] = tmp_v[...].to(v.dtype): an int64 entry takes the fp32 mean truncated
             v.copy_(out[int(plan.tens_host[k, 0]):int(plan.tens_host[k, 0]) + v.numel()].view(v.shape))
 
 
@@ -290,8 +295,9 @@ class DeviceHeteroFLMixin:
     def _hetero_names(self):
         sd = self.model.state_dict()
         for n, v in sd.items():
-            if v.dtype != torch.float32:
-                raise NotImplementedError(f"{n}: HeteroFL combination supports float32 entries (got {v.dtype})")
+            if v.dtype not in _DTYPES:
+                raise NotImplementedError(f"{n}: HeteroFL combination supports float32 and int64 entries "
+                                          f"(got {v.dtype})")
         return list(sd.keys()), [tuple(v.shape) for v in sd.values()]
 
     def client_completion_handler(self, results):

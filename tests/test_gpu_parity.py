@@ -485,3 +485,30 @@ def test_heterofl_staging_random_boxes_bit_exact(gpu_device):
     st.combine(got)
     for n in glob:
         assert torch.equal(got[n], want[n]), n
+
+
+def test_heterofl_int64_entries_follow_the_reference_cast(gpu_device):
+    """int64 state_dict entries (num_batches_tracked): the reference adds them into an fp32 tmp_v and
+    stores tmp_v / count truncated back to int64 (customized_aggregator.py:114-118)."""
+    from collections import OrderedDict
+
+    from fedscale_amd.cloud.aggregation.heterofl import combine_prefix_boxes
+    from oracle.cpu_reference import heterofl_combine
+
+    rng = np.random.default_rng(5)
+    glob = OrderedDict([("conv.weight", torch.from_numpy(rng.normal(size=(16, 8, 3, 3)).astype(np.float32))),
+                        ("bn.num_batches_tracked", torch.tensor(7, dtype=torch.int64)),
+                        ("fc.weight", torch.from_numpy(rng.normal(size=(10, 300)).astype(np.float32))),
+                        ("steps", torch.tensor([3, 9, 11], dtype=torch.int64))])
+    locs = []
+    for m in range(5):
+        locs.append(OrderedDict([("conv.weight", rng.normal(size=(16 - 2 * m, 8 - m, 3, 3)).astype(np.float32)),
+                                 ("bn.num_batches_tracked", np.array(10 + 3 * m, dtype=np.int64)),
+                                 ("fc.weight", rng.normal(size=(10, 300 - 40 * m)).astype(np.float32)),
+                                 ("steps", np.array([1 + m, 2 * m, 5], dtype=np.int64)[:3 - (m % 2)])]))
+    want = OrderedDict((n, v.clone()) for n, v in glob.items())
+    heterofl_combine(want, locs)
+    got = OrderedDict((n, v.clone()) for n, v in glob.items())
+    combine_prefix_boxes(got, locs, device=gpu_device)
+    for n in glob:
+        assert got[n].dtype == want[n].dtype and torch.equal(got[n], want[n]), n
