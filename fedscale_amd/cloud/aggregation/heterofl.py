@@ -20,7 +20,11 @@ from ... import _native as N
 from ...bucket import default_pack_workers
 
 HB_ELEMS = 1024
+FLAT_ELEMS = 4096   # FLAT mode: elements per workgroup (HB_FLAT_J x 1024 in fedagg.hip)
 ROW_MODE_MIN = 256  # rows at least this long get one workgroup per (row, 1024 columns)
+#: FLAT mode for tensors whose rows are a multiple of 4 long (False: the previous ROW / ELEMENT plan,
+#: kept for A/B timing in tools/heterofl_bench.py)
+USE_FLAT = True
 
 
 def _dims(shape):
@@ -33,8 +37,9 @@ def _dims(shape):
 
 def _box_desc(global_dims, row_mode, local_shapes, global_shapes, off: int, m: int = 0):
     """Upload descriptors {offset, o, L, ld} of ONE client's boxes starting at element ``off`` of the
-    upload buffer; returns (desc rows, next offset, data elements).  ROW-mode boxes start 16-byte aligned
-    with rows padded to a multiple of 4 elements; ELEMENT-mode boxes are packed densely."""
+    upload buffer; returns (desc rows, next offset, data elements).  Boxes of tensors read with float4
+    loads (``row_mode[k]``: ROW or FLAT mode) start 16-byte aligned with rows padded to a multiple of 4
+    elements; the others are packed densely."""
     rows, data = [], 0
     for k, (ls, gs) in enumerate(zip(local_shapes, global_shapes)):
         ls, gs = tuple(int(v) for v in ls), tuple(int(v) for v in gs)
@@ -54,9 +59,14 @@ def _box_desc(global_dims, row_mode, local_shapes, global_shapes, off: int, m: i
     return rows, off, data
 
 
+def _flat_ok(I, S):
+    return (I * S) % 4 == 0 and I * S >= 4
+
+
 def _global_dims(global_shapes):
+    """Per tensor (O, I, S) and whether its boxes use the padded 16-byte-row layout (ROW or FLAT mode)."""
     dims = [_dims(gs) for gs in global_shapes]
-    return dims, [I * S >= ROW_MODE_MIN for (_, I, S) in dims]
+    return dims, [I * S >= ROW_MODE_MIN or _flat_ok(I, S) for (_, I, S) in dims]
 
 
 _DTYPES = (torch.float32, torch.int64)  # int64 entries (BatchNorm num_batches_tracked) go through fp32
@@ -64,18 +74,23 @@ _CHUNKS: dict = {}
 
 
 def _chunk_list(global_shapes: tuple, device):
-    """Workgroup -> (tensor, row | -1) and first element, for a set of global shapes (cached on the
-    device: it depends on the model only).  ROW mode: one chunk per (row, 1024 columns); ELEMENT mode:
-    one chunk per 1024 elements of the flattened tensor."""
-    key = (global_shapes, str(device))
+    """Workgroup -> (tensor, row | -1 | -2) and first element, for a set of global shapes (cached on the
+    device: it depends on the model only).  FLAT mode (-2, rows a multiple of 4 long): one chunk per
+    4096 elements of the flattened tensor; ROW mode (other rows of >= 256): one chunk per (row, 1024
+    columns); ELEMENT mode (-1): one chunk per 1024 elements of the flattened tensor."""
+    key = (global_shapes, str(device), USE_FLAT)
     hit = _CHUNKS.get(key)
     if hit is not None:
         return hit
-    dims, row_mode = _global_dims(global_shapes)
+    dims, _ = _global_dims(global_shapes)
     cts, cfs = [], []
     for k, (O, I, S) in enumerate(dims):
         RL = I * S
-        if row_mode[k]:
+        if USE_FLAT and _flat_ok(I, S):
+            n = (O * RL + FLAT_ELEMS - 1) // FLAT_ELEMS
+            cts.append(np.stack([np.full(n, k, dtype=np.int32), np.full(n, -2, dtype=np.int32)], axis=1).reshape(-1))
+            cfs.append(np.arange(n, dtype=np.int64) * FLAT_ELEMS)
+        elif RL >= ROW_MODE_MIN:
             nch = (RL + HB_ELEMS - 1) // HB_ELEMS
             rows = np.repeat(np.arange(O, dtype=np.int32), nch)
             cts.append(np.stack([np.full(O * nch, k, dtype=np.int32), rows], axis=1).reshape(-1))

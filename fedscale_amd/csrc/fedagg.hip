@@ -996,6 +996,72 @@ __device__ __forceinline__ void hb_add(float& acc, int& cnt, float v, bool hit) 
   }
 }
 
+// FLAT mode (rows of RL % 4 == 0 elements, boxes padded to 16-byte rows): the workgroup owns HB_FLAT_J x
+// 1024 consecutive elements of the flattened tensor; thread t takes the float4 groups at
+// c0 + j*1024 + 4t, j < HB_FLAT_J (a group never straddles a row).  A full-rate client's box rows are
+// contiguous in its upload, so each client contributes HB_FLAT_J x 4 KiB of contiguous reads per
+// workgroup — longer runs per DRAM page than ROW mode's one row segment.
+#ifndef HB_FLAT_J
+#define HB_FLAT_J 4
+#endif
+#ifndef HB_FLAT_U
+#define HB_FLAT_U 2
+#endif
+__device__ __forceinline__ void prefix_box_flat(const float* __restrict__ xs, const int64_t* __restrict__ dk,
+                                                int64_t dstride, int K, int64_t goff, int64_t RL, int64_t n,
+                                                int64_t c0, float* glob) {
+  int64_t o[HB_FLAT_J], r[HB_FLAT_J];
+  bool in[HB_FLAT_J];
+#pragma unroll
+  for (int j = 0; j < HB_FLAT_J; ++j) {
+    const int64_t e = c0 + j * 1024 + 4 * (int64_t)threadIdx.x;
+    in[j] = e < n;
+    o[j] = e / RL;
+    r[j] = e - o[j] * RL;
+  }
+  float acc[HB_FLAT_J][4];
+  int cnt[HB_FLAT_J][4];
+#pragma unroll
+  for (int j = 0; j < HB_FLAT_J; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[j][i] = 0.f;  // tmp_v = v.new_zeros(..., dtype=torch.float32)
+      cnt[j][i] = 0;
+    }
+  for (int m0 = 0; m0 < K; m0 += HB_FLAT_U) {
+    f4 t[HB_FLAT_U][HB_FLAT_J];
+    int64_t len[HB_FLAT_U][HB_FLAT_J];
+#pragma unroll
+    for (int u = 0; u < HB_FLAT_U; ++u) {
+      const bool mv = m0 + u < K;
+      const int64_t* d = dk + (int64_t)(mv ? m0 + u : 0) * dstride;
+      const int64_t off = d[0], om = mv ? d[1] : 0, Lm = d[2], ldm = d[3];
+#pragma unroll
+      for (int j = 0; j < HB_FLAT_J; ++j) {
+        len[u][j] = (in[j] && o[j] < om) ? Lm : 0;  // covered columns of this row: [0, L_m)
+        t[u][j] = r[j] < len[u][j] ? hb_load(xs + off + o[j] * ldm + r[j]) : f4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < HB_FLAT_U; ++u)
+#pragma unroll
+      for (int j = 0; j < HB_FLAT_J; ++j) {
+        hb_add(acc[j][0], cnt[j][0], t[u][j].x, r[j] < len[u][j]);
+        hb_add(acc[j][1], cnt[j][1], t[u][j].y, r[j] + 1 < len[u][j]);
+        hb_add(acc[j][2], cnt[j][2], t[u][j].z, r[j] + 2 < len[u][j]);
+        hb_add(acc[j][3], cnt[j][3], t[u][j].w, r[j] + 3 < len[u][j]);
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < HB_FLAT_J; ++j) {
+    if (!in[j]) continue;
+    float* g = glob + goff + o[j] * RL + r[j];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      if (cnt[j][i] > 0) g[i] = __fdiv_rn(acc[j][i], (float)cnt[j][i]);  // tmp_v[count>0].div_(count[..])
+  }
+}
+
 __global__ __launch_bounds__(256) void k_prefix_box(const float* __restrict__ xs, const int64_t* __restrict__ desc,
                                                     int K, int T, const int64_t* __restrict__ tens,
                                                     const int32_t* __restrict__ ck_t,
@@ -1007,6 +1073,10 @@ __global__ __launch_bounds__(256) void k_prefix_box(const float* __restrict__ xs
   const int64_t RL = tens[4 * k + 2] * tens[4 * k + 3];  // global row length I*S
   const int64_t* dk = desc + 4 * (int64_t)k;
   const int64_t dstride = 4 * (int64_t)T;
+  if (row == -2) {  // FLAT mode: 4096 consecutive elements of a tensor whose rows are a multiple of 4 long
+    prefix_box_flat(xs, dk, dstride, K, goff, RL, tens[4 * k + 1] * RL, ck_first[c], glob);
+    return;
+  }
   if (row >= 0) {
     const int64_t o = row;
     const int64_t r = ck_first[c] + 4 * (int64_t)threadIdx.x;  // 4 columns per thread, 16-byte aligned

@@ -32,27 +32,41 @@ def main():
             return (s[0],) if s[0] == 10 else (math.ceil(r * s[0]),)
         return s
 
+    from fedscale_amd.cloud.aggregation import heterofl
+
+    if os.environ.get("HB_FLAT_ELEMS"):  # tuning builds with -DHB_FLAT_J=J need J*1024 here
+        heterofl.FLAT_ELEMS = int(os.environ["HB_FLAT_ELEMS"])
     lshapes = [[box(s, r, k == 0) for k, s in enumerate(gshapes)] for r in rates]
-    plan = PrefixBoxPlan(gshapes, lshapes, "cuda:0")
+    plans = {}
+    for flat in (False, True):  # A/B in one process: the ROW/ELEMENT plan, then FLAT (production)
+        heterofl.USE_FLAT = flat
+        plans[flat] = PrefixBoxPlan(gshapes, lshapes, "cuda:0")
+    plan = plans[True]
     xs = torch.empty(1, plan.upload_elems, device="cuda:0")
     synth.fill(xs, 1, plan.upload_elems, seed=9)
     xs = xs[0]
     glob = torch.empty(1, plan.P + 64, device="cuda:0")
     synth.fill(glob, 1, plan.P, seed=10)
     glob = glob[0]
-    plan.run(xs, glob)
-    torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        plan.run(xs, glob)
-    e1.record()
-    torch.cuda.synchronize()
-    ms = e0.elapsed_time(e1) / reps
+    ms = {False: [], True: []}
+    for rnd in range(3):
+        for flat, pl in plans.items():
+            pl.run(xs, glob)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(reps):
+                pl.run(xs, glob)
+            e1.record()
+            torch.cuda.synchronize()
+            ms[flat].append(e0.elapsed_time(e1) / reps)
     alg = 4 * plan.upload_data_elems + 8 * plan.P  # every uploaded parameter read once; global read + written
+    m = float(np.median(ms[True]))
+    m_row = float(np.median(ms[False]))
     out = {"K": K, "P": plan.P, "upload_elems": plan.upload_data_elems, "padded_elems": plan.upload_elems,
-           "kernel_ms": ms,
-           "GBps": alg / (ms * 1e-3) / 1e9, "client_updates_per_s": K / (ms * 1e-3)}
+           "kernel_ms": m, "GBps": alg / (m * 1e-3) / 1e9, "client_updates_per_s": K / (m * 1e-3),
+           "chunks": plan.nchunks, "row_plan_kernel_ms": m_row, "row_plan_GBps": alg / (m_row * 1e-3) / 1e9,
+           "row_plan_chunks": plans[False].nchunks}
     print(json.dumps(out))
     json.dump(out, open(os.path.join(ROOT, "gpurun_out", "heterofl_bench.json"), "w"), indent=1)
 
