@@ -20,7 +20,7 @@ from ... import _native as N
 from ...bucket import default_pack_workers
 
 HB_ELEMS = 1024
-FLAT_ELEMS = 4096   # FLAT mode: elements per workgroup (HB_FLAT_J x 1024 in fedagg.hip)
+FLAT_ELEMS = 8192   # FLAT mode: elements per workgroup (HB_FLAT_J x 1024 in fedagg.hip)
 ROW_MODE_MIN = 256  # rows at least this long get one workgroup per (row, 1024 columns)
 #: FLAT mode for tensors whose rows are a multiple of 4 long (False: the previous ROW / ELEMENT plan,
 #: kept for A/B timing in tools/heterofl_bench.py)
@@ -76,9 +76,9 @@ _CHUNKS: dict = {}
 def _chunk_list(global_shapes: tuple, device):
     """Workgroup -> (tensor, row | -1 | -2) and first element, for a set of global shapes (cached on the
     device: it depends on the model only).  FLAT mode (-2, rows a multiple of 4 long): one chunk per
-    4096 elements of the flattened tensor; ROW mode (other rows of >= 256): one chunk per (row, 1024
+    FLAT_ELEMS elements of the flattened tensor; ROW mode (other rows of >= 256): one chunk per (row, 1024
     columns); ELEMENT mode (-1): one chunk per 1024 elements of the flattened tensor."""
-    key = (global_shapes, str(device), USE_FLAT)
+    key = (global_shapes, str(device), USE_FLAT, FLAT_ELEMS)
     hit = _CHUNKS.get(key)
     if hit is not None:
         return hit

@@ -1002,10 +1002,10 @@ __device__ __forceinline__ void hb_add(float& acc, int& cnt, float v, bool hit) 
 // contiguous in its upload, so each client contributes HB_FLAT_J x 4 KiB of contiguous reads per
 // workgroup — longer runs per DRAM page than ROW mode's one row segment.
 #ifndef HB_FLAT_J
-#define HB_FLAT_J 4
+#define HB_FLAT_J 8
 #endif
 #ifndef HB_FLAT_U
-#define HB_FLAT_U 2
+#define HB_FLAT_U 1
 #endif
 __device__ __forceinline__ void prefix_box_flat(const float* __restrict__ xs, const int64_t* __restrict__ dk,
                                                 int64_t dstride, int K, int64_t goff, int64_t RL, int64_t n,
@@ -1062,18 +1062,17 @@ __device__ __forceinline__ void prefix_box_flat(const float* __restrict__ xs, co
   }
 }
 
-__global__ __launch_bounds__(256) void k_prefix_box(const float* __restrict__ xs, const int64_t* __restrict__ desc,
-                                                    int K, int T, const int64_t* __restrict__ tens,
-                                                    const int32_t* __restrict__ ck_t,
-                                                    const int64_t* __restrict__ ck_first, float* glob) {
-  const int c = blockIdx.x;
+__device__ __forceinline__ void prefix_box_chunk(const float* __restrict__ xs, const int64_t* __restrict__ desc,
+                                                 int K, int T, const int64_t* __restrict__ tens,
+                                                 const int32_t* __restrict__ ck_t,
+                                                 const int64_t* __restrict__ ck_first, float* glob, int c) {
   const int k = ck_t[2 * c];
   const int row = ck_t[2 * c + 1];
   const int64_t goff = tens[4 * k];
   const int64_t RL = tens[4 * k + 2] * tens[4 * k + 3];  // global row length I*S
   const int64_t* dk = desc + 4 * (int64_t)k;
   const int64_t dstride = 4 * (int64_t)T;
-  if (row == -2) {  // FLAT mode: 4096 consecutive elements of a tensor whose rows are a multiple of 4 long
+  if (row == -2) {  // FLAT mode: HB_FLAT_J x 1024 consecutive elements, rows a multiple of 4 long
     prefix_box_flat(xs, dk, dstride, K, goff, RL, tens[4 * k + 1] * RL, ck_first[c], glob);
     return;
   }
@@ -1146,6 +1145,17 @@ __global__ __launch_bounds__(256) void k_prefix_box(const float* __restrict__ xs
   }
 }
 
+// HB_GRID > 0 caps the grid; workgroup b then takes chunks b, b + grid, ... (fewer concurrent streams)
+#ifndef HB_GRID
+#define HB_GRID 0
+#endif
+__global__ __launch_bounds__(256) void k_prefix_box(const float* __restrict__ xs, const int64_t* __restrict__ desc,
+                                                    int K, int T, const int64_t* __restrict__ tens,
+                                                    const int32_t* __restrict__ ck_t,
+                                                    const int64_t* __restrict__ ck_first, float* glob, int nchunks) {
+  for (int c = blockIdx.x; c < nchunks; c += gridDim.x) prefix_box_chunk(xs, desc, K, T, tens, ck_t, ck_first, glob, c);
+}
+
 extern "C" int fa_prefix_box_combine(const float* xs, const int64_t* desc, int32_t K, const int64_t* tensors,
                                      int32_t T, const int32_t* chunk_tensor, const int64_t* chunk_first,
                                      int32_t nchunks, float* global, fa_stream_t stream) {
@@ -1154,8 +1164,9 @@ extern "C" int fa_prefix_box_combine(const float* xs, const int64_t* desc, int32
   if (!xs || !desc || !tensors || !chunk_tensor || !chunk_first || !global)
     return fail(FA_E_ARG, "fa_prefix_box_combine: NULL pointer");
   if (!aligned16(xs)) return fail(FA_E_ARG, "fa_prefix_box_combine: xs must be 16-byte aligned");
-  hipLaunchKernelGGL(k_prefix_box, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, xs, desc, (int)K, (int)T, tensors,
-                     chunk_tensor, chunk_first, global);
+  const int grid = (HB_GRID > 0 && nchunks > HB_GRID) ? HB_GRID : nchunks;
+  hipLaunchKernelGGL(k_prefix_box, dim3(grid), dim3(256), 0, (hipStream_t)stream, xs, desc, (int)K, (int)T, tensors,
+                     chunk_tensor, chunk_first, global, (int)nchunks);
   return check_launch("fa_prefix_box_combine");
 }
 

@@ -158,7 +158,7 @@ int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uint32_t seed,
  *   tensors  [T][4] = {offset in global, O, I, S};  chunk_tensor[2c] = tensor of workgroup c,
  *            chunk_tensor[2c+1] = row o (>= 0: columns [chunk_first[c], +1024) of that row, chunk_first
  *            a multiple of 4), -1 (elements [chunk_first[c], +1024) of the flattened tensor, any layout)
- *            or -2 (FLAT: elements [chunk_first[c], +4096) of the flattened tensor; I*S a multiple of 4,
+ *            or -2 (FLAT: elements [chunk_first[c], +8192) of the flattened tensor; I*S a multiple of 4,
  *            chunk_first a multiple of 4, boxes in the padded ROW layout)
  * global[e] <- (sum over covering clients, client order, fp32 from 0) / fp32(count) where count > 0.
  */
