@@ -105,10 +105,13 @@ class BucketLayout:
 
         The fp32 byte ranges go to ``fa_host_gather`` (native, multi-threaded memcpy into the pinned row):
         a single memcpy stream is slower than the H2D copy engine."""
-        from . import _native
+        self.run_host_gather(self.host_gather_plan(values), f_out, i_out, workers)
 
+    def host_gather_plan(self, values: list):
+        """Validate an update (shapes, dtypes) and list its byte ranges for ``run_host_gather``: the cheap,
+        synchronous half of pack_host (the caller's errors surface here, at the add, as in the reference)."""
         values = self.values_of(values)
-        srcs, offs, sizes, keep = [], [], [], []
+        srcs, offs, sizes, keep, side = [], [], [], [], []
         for e in self.entries:
             v = values[e.index]
             if isinstance(v, torch.Tensor):
@@ -129,15 +132,22 @@ class BucketLayout:
             else:
                 if a.dtype != np.int64:
                     raise TypeError(f"{e.name}: dtype {a.dtype}, the model entry is int64")
-                i_out[e.offset:e.offset + e.numel] = a.reshape(-1)
+                side.append((e.offset, a.reshape(-1)))
+        return (np.asarray(srcs, dtype=np.uint64), np.asarray(offs, dtype=np.int64),
+                np.asarray(sizes, dtype=np.int64), keep, side)
+
+    def run_host_gather(self, plan, f_out: np.ndarray, i_out: np.ndarray, workers: int = 1):
+        """The copying half of pack_host (no Python-level validation left; releases the GIL in C)."""
+        from . import _native
+
+        ps, po, pn, keep, side = plan
         if not f_out.flags.c_contiguous or f_out.dtype != np.float32 or f_out.size < self.P:
             raise ValueError("pack_host: f_out must be a contiguous float32 array of >= P elements")
-        if srcs:
-            ps = np.asarray(srcs, dtype=np.uint64)
-            po = np.asarray(offs, dtype=np.int64)
-            pn = np.asarray(sizes, dtype=np.int64)
+        for off, a in side:
+            i_out[off:off + a.size] = a
+        if len(ps):
             _native.call("fa_host_gather", f_out.ctypes.data, ps.ctypes.data, po.ctypes.data, pn.ctypes.data,
-                         len(srcs), int(workers))
+                         len(ps), int(workers))
         del keep
 
     def pack_device(self, values: list, f_dst: torch.Tensor, i_dst: torch.Tensor):
@@ -172,11 +182,17 @@ class ClientStaging:
     """Device staging area for up to ``capacity`` client updates of one round (chunk).
 
     Host -> device ingress goes through a ring of pinned host buffers; each H2D copy is enqueued on the
-    current stream, so stream order guarantees a slot is not overwritten while a kernel still reads it.
+    caller's current stream, so stream order guarantees a slot is not overwritten while a kernel still
+    reads it.  With ``async_ingress`` the gather into the pinned row and the H2D enqueue run on one
+    background thread, in arrival order: ``put`` validates the update and returns.  It is off by default:
+    measured with the executor's pickled payloads, the background copy and the main thread's
+    ``pickle.loads`` (aggregator.py:704) serialise on the GIL and halve the rate.
+    ``drain()`` waits for every queued copy to be enqueued; DeviceRound calls it before any kernel reads
+    the slots.
     """
 
     def __init__(self, layout: BucketLayout, device, capacity: int, ring: int = 2,
-                 pack_workers: Optional[int] = None):
+                 pack_workers: Optional[int] = None, async_ingress: bool = False):
         self.layout = layout
         self.pack_workers = pack_workers or default_pack_workers()
         self.device = torch.device(device)
@@ -188,24 +204,51 @@ class ClientStaging:
         for _ in range(ring):
             hf = torch.zeros(layout.ld, dtype=torch.float32).pin_memory()
             hi = torch.zeros(layout.ldq, dtype=torch.int64).pin_memory()
-            self._ring.append([hf, hi, None])
+            self._ring.append([hf, hi, None, None])  # pinned rows, event of the last H2D, pending job
         self._next = 0
+        self.async_ingress = async_ingress
+        self._pool = None
+
+    def _copy_in(self, slot, plan, hf, hi, stream):
+        lay = self.layout
+        lay.run_host_gather(plan, hf.numpy(), hi.numpy(), workers=self.pack_workers)
+        with torch.cuda.stream(stream):
+            self.x[slot, :lay.P].copy_(hf[:lay.P], non_blocking=True)
+            if lay.Q:
+                self.xi[slot, :lay.Q].copy_(hi[:lay.Q], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+        return ev
 
     def put(self, slot: int, update):
         lay = self.layout
         values = lay.values_of(update)
         on_dev = [isinstance(v, torch.Tensor) and v.device == self.device for v in values]
         if all(on_dev):
+            self.drain()  # keep the slots' arrival order with any queued host copies
             lay.pack_device(values, self.x[slot], self.xi[slot])
             return
-        hf, hi, ev = self._ring[self._next]
-        if ev is not None:
-            ev.synchronize()  # the previous H2D out of this pinned buffer has completed
-        lay.pack_host(values, hf.numpy(), hi.numpy(), workers=self.pack_workers)
-        self.x[slot, :lay.P].copy_(hf[:lay.P], non_blocking=True)
-        if lay.Q:
-            self.xi[slot, :lay.Q].copy_(hi[:lay.Q], non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self.device))
-        self._ring[self._next][2] = ev
+        plan = lay.host_gather_plan(values)  # validation errors surface here, synchronously
+        r = self._ring[self._next]
+        if r[3] is not None:  # the job that last used this pinned row
+            r[2] = r[3].result()
+            r[3] = None
+        if r[2] is not None:
+            r[2].synchronize()  # the previous H2D out of this pinned row has completed
+        stream = torch.cuda.current_stream(self.device)
+        if self.async_ingress:
+            if self._pool is None:
+                from concurrent.futures import ThreadPoolExecutor
+
+                self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="fedagg-ingress")
+            r[3] = self._pool.submit(self._copy_in, slot, plan, r[0], r[1], stream)
+        else:
+            r[2] = self._copy_in(slot, plan, r[0], r[1], stream)
         self._next = (self._next + 1) % len(self._ring)
+
+    def drain(self):
+        """Wait until every queued copy has been enqueued on its stream (re-raising a copy's error)."""
+        for r in self._ring:
+            if r[3] is not None:
+                r[2] = r[3].result()
+                r[3] = None

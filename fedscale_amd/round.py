@@ -132,6 +132,7 @@ class DeviceRound:
 
     def _fold_chunk(self):
         """Fold the staged chunk into the running state (not the last chunk of the round)."""
+        self.staging.drain()
         L, st, n = self.layout, self.staging, self.slot
         first = self.chunks_done == 0
         if self.policy in ("fedavg", "fedbuff"):
@@ -190,6 +191,7 @@ class DeviceRound:
         yogi       -> dict(last=, m=, v=, eta=, tau=, beta=, omb=, omb2=, init=)
         """
         self._check_complete()
+        self.staging.drain()
         if self.cg is not None:
             return self._finalize_mean_clients(denom32, denom64, out, cur_side, model_side, yogi)
         L, st, n = self.layout, self.staging, self.slot
@@ -214,6 +216,7 @@ class DeviceRound:
             return False  # client mode: each rank holds only its block of the updates
         if self.cap < self.K or self.staging.generation != self.generation or self.n != self.K:
             return False  # some updates were overwritten by later chunks, or the slots were reused
+        self.staging.drain()
         L, st = self.layout, self.staging
         kx.reduce(st.x, self.K, L.P, out, denom=float(np.float32(self.K)), finalize=True)
         acc_i = torch.zeros(L.ldq, dtype=torch.int64, device=self.device)
