@@ -35,6 +35,23 @@ if [[ $STAGE == pmc ]]; then
   rm -f profiles/pmc_traffic.json
   python tools/pmc_parse.py $OUT/pmc_fetch $OUT/pmc_write fedavg_k1000_p25000000 $((4*1000*25000000 + 4*25000000)) && cp profiles/pmc_traffic.json $OUT/
 fi
+if [[ $STAGE == pmcpol ]]; then  # the other server steps' dominant kernels (bench --policy ...)
+  export TMPDIR=/tmp
+  K=1000; P=25000000
+  rm -f profiles/pmc_traffic.json
+  for pol in fedbuff fedyogi qfedavg; do
+    ARGS="--policy $pol --steps 3 --warmup 1 --cpu-seconds 0 --no-other-configs"
+    timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/pmc_fetch_$pol -o run -- python3 $ROOT/bench.py $ARGS > $OUT/pmc_fetch_$pol.log 2>&1 || { tail -20 $OUT/pmc_fetch_$pol.log; exit 1; }
+    timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/pmc_write_$pol -o run -- python3 $ROOT/bench.py $ARGS > $OUT/pmc_write_$pol.log 2>&1 || { tail -20 $OUT/pmc_write_$pol.log; exit 1; }
+    case $pol in
+      fedbuff) ALG=$((4*K*P + 4*P + 4*K)); KERN=k_reduce ;;
+      fedyogi) ALG=$((4*K*P + 24*P)); KERN=k_reduce ;;
+      qfedavg) ALG=$((4*K*P + 8*P + 8*K)); KERN=k_qfed_accum ;;
+    esac
+    python tools/pmc_parse.py $OUT/pmc_fetch_$pol $OUT/pmc_write_$pol ${pol}_k${K}_p${P} $ALG $KERN || exit 1
+  done
+  cp profiles/pmc_traffic.json $OUT/pmc_traffic_policies.json
+fi
 if [[ $STAGE == tune ]]; then
   timeout -k 10 300 python tools/hbm_ceiling.py 64 > $OUT/ceiling.log 2>&1 || { tail -20 $OUT/ceiling.log; exit 1; }
   cat $OUT/ceiling.log
