@@ -30,6 +30,9 @@ class DeviceAggregatorMixin:
     device_round_capacity = None
     #: keep the FedAvg mean as ``model_weights`` in fused fed-yogi rounds (costs P*4 bytes of writes)
     device_keep_mean = True
+    #: unpickle executor payloads without copying their arrays (fedscale_amd/ingress.py); the arrays of
+    #: ``update_weight`` are then read-only views of the payload
+    device_zero_copy_ingress = True
 
     _device_round = None
 
@@ -59,6 +62,23 @@ class DeviceAggregatorMixin:
     def _device_policy(self) -> str:
         opt = self._wrapper().optimizer
         return "qfedavg" if (opt is not None and getattr(opt, "mode", None) == "q-fedavg") else "fedavg"
+
+    def deserialize_response(self, responses):
+        """aggregator.py:695-704 (``pickle.loads``) without the copy of every array's bytes: the same
+        object tree, large arrays as read-only views of ``responses`` (fedscale_amd/ingress.py)."""
+        sup = getattr(super(), "deserialize_response", None)
+        # only in place of the plain pickle.loads: a subclass that converts the payload (the TFLite / MNN
+        # aggregators, aggregator_tflite.py:47-58) keeps its own path
+        plain = sup is None or getattr(sup, "__qualname__", "") == "Aggregator.deserialize_response"
+        if self.device_zero_copy_ingress and plain and type(responses) is bytes:
+            from ...ingress import loads
+
+            return loads(responses)
+        if sup is not None:
+            return sup(responses)
+        import pickle
+
+        return pickle.loads(responses)
 
     def serialize_response(self, responses):
         """aggregator.py:706-715 (``pickle.dumps``), with the global model's bytes made once per model

@@ -175,6 +175,20 @@ int fa_prefix_box_combine(const float* xs, const int64_t* desc, int32_t K, const
 int fa_host_gather(void* dst, const void* const* srcs, const int64_t* dst_off, const int64_t* nbytes, int32_t n,
                    int32_t threads);
 
+/*
+ * Host ingress (no GPU work): strip the large byte strings out of a pickled executor result so it can be
+ * unpickled without copying them (replaces the copies inside pickle.loads of deserialize_response,
+ * aggregator.py:704, on payloads made by pickle.dumps at torch_client.py:79-91).  Walks the opcode
+ * stream of `in[0:n)` up to STOP: FRAME opcodes are dropped; every BINBYTES / BINBYTES8 argument of at
+ * least `min_bytes` (>= 16) bytes is replaced by SHORT_BINBYTES of 12 bytes "FAPB" + uint64 LE region
+ * index, and regions[2r], regions[2r+1] receive the raw bytes' offset in `in` and their length (for
+ * r < max_regions).  Everything else is copied verbatim.  Returns the length of the stripped stream (it
+ * is written only when it fits in out_cap; out may be NULL to size it) and sets *nregions, or a negative
+ * FA_E* code for an unknown opcode (protocol 5 out-of-band buffers included) or a truncated stream.
+ */
+int64_t fa_pickle_strip(const uint8_t* in, int64_t n, int64_t min_bytes, uint8_t* out, int64_t out_cap,
+                        int64_t* regions, int32_t max_regions, int32_t* nregions);
+
 #ifdef __cplusplus
 }
 #endif

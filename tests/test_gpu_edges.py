@@ -154,3 +154,42 @@ def test_async_ingress_staging_matches_reference(gpu_device, name):
             assert_state_close(got, sc.expected(r), 1e-5, f"{name} r{r}", int_slack=1)
         else:
             assert_state_equal(got, sc.expected(r), f"{name} r{r}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["fedavg_femnist_cnn_k10", "fedavg_wide_k64", "fedyogi_wide_3rounds"])
+def test_zero_copy_payload_ingress_matches_reference(gpu_device, name, monkeypatch):
+    """Executor payloads (pickle.dumps of the result, torch_client.py:76-91) through the mixin's
+    deserialize_response (fedscale_amd/ingress.py: arrays as read-only views of the payload) into the
+    device round: results stay those of the reference fixture, and the fast path really ran."""
+    import pickle
+
+    from fedscale_amd import ingress
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+    from tests.golden_io import Scenario, StateDictModule, assert_state_close, assert_state_equal
+
+    monkeypatch.setattr(ingress, "MIN_BYTES", 256)  # strip every array that pickles as BINBYTES (>= 256 B)
+    sc = Scenario(name)
+    args = sc.args()
+    opt = TorchServerOptimizer(args.gradient_policy, args, "cuda:0") if sc.meta.get("optimizer") else None
+    adapter = TorchModelAdapter(StateDictModule(sc.names, sc.init_state()), optimizer=opt, device="cuda:0")
+    agg = DeviceAggregator(adapter, args)
+    policy = sc.meta["policy"]
+    for r, ks in sc.rounds():
+        if policy == "q-fedavg":
+            args.learning_rate = sc.meta["lrs"][r]
+        agg.start_round(len(ks))
+        for res in sc.results(ks, r):
+            got_res = agg.deserialize_response(pickle.dumps(res))
+            uw = got_res["update_weight"]
+            views = [v for v in (uw.values() if isinstance(uw, dict) else uw)
+                     if isinstance(v, np.ndarray) and v.nbytes >= 256]
+            assert views and all(not v.flags.writeable for v in views)
+            agg.on_result(got_res)
+        got = adapter.get_weights()
+        if policy == "fed-yogi":  # the sqrt of the reference's torch CPU path: within 1e-5 (north_star)
+            assert_state_close(got, sc.expected(r), 1e-5, f"{name} r{r}")
+        else:
+            assert_state_equal(got, sc.expected(r), f"{name} r{r}")

@@ -1,0 +1,164 @@
+"""Zero-copy payload ingress (fedscale_amd/ingress.py + fa_pickle_strip): ``ingress.loads`` must return
+what ``pickle.loads`` returns (aggregator.py:704) for every payload the executor can send
+(torch_client.py:76-91), and fall back to ``pickle.loads`` for anything else.  Host-only code: runs on CPU."""
+import ctypes
+import pickle
+
+import numpy as np
+import pytest
+
+from fedscale_amd import _native, ingress
+
+
+def _assert_same(a, b, path="root"):
+    assert type(a) is type(b), path
+    if isinstance(a, np.ndarray):
+        assert a.dtype == b.dtype and a.shape == b.shape, path
+        assert a.flags.f_contiguous == b.flags.f_contiguous and a.flags.c_contiguous == b.flags.c_contiguous
+        assert a.tobytes() == b.tobytes(), path  # bitwise (NaN payloads included)
+    elif isinstance(a, dict):
+        assert list(a.keys()) == list(b.keys()), path
+        for k in a:
+            _assert_same(a[k], b[k], f"{path}.{k}")
+    elif isinstance(a, (list, tuple)):
+        assert len(a) == len(b), path
+        for i, (x, y) in enumerate(zip(a, b)):
+            _assert_same(x, y, f"{path}[{i}]")
+    else:
+        assert a == b or (a != a and b != b), path
+
+
+def _executor_result(seed=0, scale=1):
+    """Shape of torch_client.py:76-91's result for a small ResNet-like state_dict."""
+    rng = np.random.default_rng(seed)
+    w = {}
+    for i in range(6):
+        w[f"layer{i}.conv.weight"] = rng.standard_normal((16 * scale, 8, 3, 3), dtype=np.float32)
+        w[f"layer{i}.bn.weight"] = rng.standard_normal(16 * scale, dtype=np.float32)
+        w[f"layer{i}.bn.running_var"] = rng.random(16 * scale, dtype=np.float32)
+        w[f"layer{i}.bn.num_batches_tracked"] = np.array(7 + i, dtype=np.int64)
+    w["fc.weight"] = rng.standard_normal((10, 512 * scale), dtype=np.float32)
+    w["fc.weight"][0, :4] = [np.nan, np.inf, -np.inf, -0.0]
+    return {"client_id": 3 + seed, "moving_loss": 1.25, "trained_size": 200, "success": True,
+            "utility": 17.5, "update_weight": w, "wall_duration": 0}
+
+
+def test_executor_result_roundtrip():
+    r = _executor_result()
+    b = pickle.dumps(r)
+    got = ingress.loads(b)
+    _assert_same(got, pickle.loads(b))
+    # large arrays really are views of the payload (no copy), small ones are rebuilt inline
+    big = got["update_weight"]["layer0.conv.weight"]
+    assert not big.flags.writeable and big.base is not None
+    assert got["update_weight"]["layer0.bn.num_batches_tracked"].flags.writeable
+
+
+def test_strip_regions_point_at_array_bytes():
+    r = _executor_result(seed=1)
+    b = pickle.dumps(r)
+    stream, regions = ingress.strip(b, ingress.MIN_BYTES)
+    big = [a for a in r["update_weight"].values() if a.nbytes >= ingress.MIN_BYTES]
+    assert len(regions) == len(big)
+    for a, (off, n) in zip(big, regions):
+        assert n == a.nbytes and b[off:off + n] == a.tobytes()
+    assert len(stream) < len(b) - sum(a.nbytes for a in big) + 14 * len(big)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.float16, np.int64, np.int32, np.uint8, np.bool_,
+                                   np.complex64])
+def test_dtypes_and_layouts(dtype):
+    rng = np.random.default_rng(2)
+    base = (rng.standard_normal((70, 90)) * 50)
+    a = base.astype(dtype) if dtype is not np.complex64 else (base + 1j * base).astype(dtype)
+    obj = {"c": np.ascontiguousarray(a), "f": np.asfortranarray(a), "t": a.T, "s": a[::2, 1:],
+           "e": np.empty((0, 5000), dtype), "z": np.zeros((64, 64), dtype)}
+    b = pickle.dumps(obj)
+    _assert_same(ingress.loads(b, min_bytes=64), pickle.loads(b))
+
+
+def test_nested_containers_and_shared_arrays():
+    a = np.arange(20000, dtype=np.float32)
+    obj = {"l": [a, (a, 1.0), {"x": a}], "t": (np.ones(5000, np.int64), "s"), "k": [[np.zeros(3000)]]}
+    b = pickle.dumps(obj)
+    got = ingress.loads(b)
+    _assert_same(got, pickle.loads(b))
+    # memoised once in the pickle -> one object after loading, as with pickle.loads
+    assert got["l"][0] is got["l"][1][0] is got["l"][2]["x"]
+
+
+@pytest.mark.parametrize("case", ["bytes_blob", "object_array", "subclass", "custom_object", "protocol2",
+                                  "protocol5", "small", "bytearray"])
+def test_fallback_cases_match_pickle(case):
+    big = np.arange(10000, dtype=np.float32)
+    if case == "bytes_blob":
+        obj = {"w": big, "blob": b"\x01" * 10000}
+    elif case == "object_array":
+        obj = {"w": big, "o": np.array([{"a": 1}, "x", 3.0] * 2000, dtype=object)}
+    elif case == "subclass":
+        obj = {"w": big, "m": np.ma.masked_array(big, mask=big > 5000)}
+    elif case == "custom_object":
+        import collections
+
+        obj = {"w": collections.OrderedDict(a=big)}
+    elif case == "small":
+        obj = {"w": np.arange(10, dtype=np.float32)}
+    elif case == "bytearray":
+        obj = {"w": big, "b": bytearray(b"\x02" * 9000)}
+    else:
+        obj = {"w": big, "n": 3}
+    proto = {"protocol2": 2, "protocol5": 5}.get(case, 4)
+    b = pickle.dumps(obj, protocol=proto)
+    got, ref = ingress.loads(b), pickle.loads(b)
+    assert type(got) is type(ref) and list(got) == list(ref)
+    assert pickle.dumps(got, protocol=4) == pickle.dumps(ref, protocol=4)
+
+
+def test_truncated_payload_raises_like_pickle():
+    b = pickle.dumps(_executor_result())
+    for cut in (len(b) // 2, len(b) - 1):
+        with pytest.raises(Exception) as ref:
+            pickle.loads(b[:cut])
+        with pytest.raises(type(ref.value)):
+            ingress.loads(b[:cut])
+
+
+def test_strip_error_paths():
+    lib = _native.load()
+    n = ctypes.c_int32(0)
+    regions = (ctypes.c_int64 * 8)()
+    good = pickle.dumps({"w": np.ones(5000, np.float32)})
+    assert lib.fa_pickle_strip(good, len(good), 8, None, 0, regions, 4, ctypes.byref(n)) < 0   # min_bytes < 16
+    assert lib.fa_pickle_strip(good, len(good) - 1, 64, None, 0, regions, 4, ctypes.byref(n)) < 0  # no STOP
+    p5 = pickle.dumps(pickle.PickleBuffer(np.ones(100, np.uint8)), protocol=5, buffer_callback=lambda _: False)
+    assert lib.fa_pickle_strip(p5, len(p5), 64, None, 0, regions, 4, ctypes.byref(n)) < 0  # out-of-band
+    # sizing call (out=NULL) reports the exact stripped length; the second call fills it
+    need = lib.fa_pickle_strip(good, len(good), 64, None, 0, regions, 4, ctypes.byref(n))
+    assert need > 0 and n.value == 1
+    out = ctypes.create_string_buffer(need)
+    assert lib.fa_pickle_strip(good, len(good), 64, out, need, regions, 4, ctypes.byref(n)) == need
+    assert out.raw.count(b"FAPB") == 1 and regions[1] == 20000
+
+
+def test_aggregator_deserialize_hook():
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregatorMixin
+
+    class Base:
+        def deserialize_response(self, responses):
+            return ("converted", pickle.loads(responses))
+
+    class Plain(DeviceAggregatorMixin):
+        pass
+
+    class Converting(DeviceAggregatorMixin, Base):
+        pass
+
+    b = pickle.dumps(_executor_result(scale=4))
+    got = Plain().deserialize_response(b)
+    _assert_same(got, pickle.loads(b))
+    assert not got["update_weight"]["fc.weight"].flags.writeable
+    # a base class that converts the payload keeps its own path
+    assert Converting().deserialize_response(b)[0] == "converted"
+    off = Plain()
+    off.device_zero_copy_ingress = False
+    assert off.deserialize_response(b)["update_weight"]["fc.weight"].flags.writeable

@@ -26,6 +26,8 @@ def main():
     allout = [run(K, rounds, which, w) for w in worker_list]
     # full ingress from the executor's pickled payload (aggregator.py:704 deserialize_response)
     allout.append(run(K, rounds, which, None, loader="pickle"))
+    # the mixin's deserialize_response: the same payload without copying its arrays (fedscale_amd/ingress.py)
+    allout.append(run(K, rounds, which, None, loader="zerocopy"))
     allout.append(egress(which))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(allout, open(os.path.join(ROOT, "gpurun_out", f"ingress_{which}_k{K}.json"), "w"), indent=1)
@@ -60,8 +62,10 @@ def run(K, rounds, which, workers, loader=None):
     if loader is not None:
         import pickle
 
-        payloads = [pickle.dumps({"client_id": i, "update_weight": d, "moving_loss": 1.0}) for i, d in enumerate(pool)]
-        load = pickle.loads
+        payloads = [pickle.dumps({"client_id": i, "moving_loss": 1.0, "trained_size": 200, "success": True,
+                                  "utility": 1.0, "update_weight": d, "wall_duration": 0})
+                    for i, d in enumerate(pool)]
+        load = pickle.loads if loader == "pickle" else agg.deserialize_response
         t0 = time.perf_counter()
         for r in range(16):
             load(payloads[r % 8])
