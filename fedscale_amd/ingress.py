@@ -25,13 +25,15 @@ from __future__ import annotations
 
 import ctypes
 import io
+import math
 import pickle
 
 import numpy as np
 
 from . import _native
 
-#: byte strings shorter than this stay inline (small tensors, strings, scalars)
+#: byte strings shorter than this stay inline (small tensors, strings, scalars): below a few KiB numpy's
+#: own rebuild (C) is cheaper than a view built in Python (measured on a ResNet-18 payload)
 MIN_BYTES = 4096
 
 _TAG = b"FAPB"
@@ -92,12 +94,12 @@ class _Materializer:
             if idx >= len(self.regions):
                 raise _Fallback("tag index out of range")
             off, n = self.regions[idx]
-            count = int(np.prod(shape, dtype=np.int64)) if len(shape) else 1
+            count = math.prod(shape)
             if count * dtype.itemsize != n:
                 raise _Fallback("tagged byte count does not match the array")
             self.used += 1
             a = np.frombuffer(self.payload, dtype=dtype, count=count, offset=off)
-            return a.reshape(shape, order="F" if fortran else "C")
+            return a.reshape(shape, order="F") if fortran else a.reshape(shape)
         a = stub.reconstruct(*stub.args)  # exactly what pickle.loads does for an inline array
         a.__setstate__(st)
         return a
