@@ -33,6 +33,9 @@ class DeviceAggregatorMixin:
     #: unpickle executor payloads without copying their arrays (fedscale_amd/ingress.py); the arrays of
     #: ``update_weight`` are then read-only views of the payload
     device_zero_copy_ingress = True
+    #: create_client_task / get_test_config hand the servicer an EgressHandle (the cached pickled bytes of
+    #: the model version) instead of a fresh clone of the model per request
+    device_egress_handles = True
 
     _device_round = None
 
@@ -69,8 +72,8 @@ class DeviceAggregatorMixin:
         sup = getattr(super(), "deserialize_response", None)
         # only in place of the plain pickle.loads: a subclass that converts the payload (the TFLite / MNN
         # aggregators, aggregator_tflite.py:47-58) keeps its own path
-        plain = sup is None or getattr(sup, "__qualname__", "") == "Aggregator.deserialize_response"
-        if self.device_zero_copy_ingress and plain and type(responses) is bytes:
+        if self.device_zero_copy_ingress and self._reference_impl("deserialize_response") and \
+                type(responses) is bytes:
             from ...ingress import loads
 
             return loads(responses)
@@ -84,6 +87,9 @@ class DeviceAggregatorMixin:
         """aggregator.py:706-715 (``pickle.dumps``), with the global model's bytes made once per model
         version: the reference pickles get_weights() again for every executor request
         (create_client_task :804, get_test_config :816, UPDATE_MODEL :903)."""
+        payload = getattr(responses, "egress_payload", None)
+        if type(payload) is bytes:  # an EgressHandle: the bytes of its own model version
+            return payload
         key = getattr(responses, "egress_key", None)
         if key is not None:
             wrappers = self.model_wrapper if isinstance(self.model_wrapper, list) else [self.model_wrapper]
@@ -98,6 +104,36 @@ class DeviceAggregatorMixin:
         import pickle
 
         return pickle.dumps(responses)
+
+    def _reference_impl(self, name) -> bool:
+        """True when the next ``name`` in the MRO is the reference Aggregator's own (a plugin that
+        overrides it, e.g. Auxo's create_client_task, keeps its version)."""
+        sup = getattr(super(), name, None)
+        return sup is None or getattr(sup, "__qualname__", "").split(".")[-2:] == ["Aggregator", name]
+
+    def _egress_weights(self):
+        """``self.model_wrapper.get_weights()`` as the servicer uses it (serialised, :905-907): an
+        EgressHandle on the cached bytes of this model version instead of a clone of the model."""
+        w = self.model_wrapper
+        if self.device_egress_handles and isinstance(w, TorchModelAdapter):
+            return w.egress_handle()
+        return w.get_weights()
+
+    def create_client_task(self, executor_id):
+        """aggregator.py:788-804 with the weights handed over as an EgressHandle (``_egress_weights``)."""
+        if not self._reference_impl("create_client_task"):
+            return super().create_client_task(executor_id)
+        next_client_id = self.resource_manager.get_next_task(executor_id)
+        train_config = None
+        if next_client_id is not None:
+            train_config = {"client_id": next_client_id, "task_config": self.get_client_conf(next_client_id)}
+        return train_config, self._egress_weights()
+
+    def get_test_config(self, client_id):
+        """aggregator.py:806-816 with the weights handed over as an EgressHandle."""
+        if not self._reference_impl("get_test_config"):
+            return super().get_test_config(client_id)
+        return {"client_id": client_id}, self._egress_weights()
 
     def update_weight_aggregation(self, results):
         w = self._wrapper()

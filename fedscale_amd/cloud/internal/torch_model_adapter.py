@@ -42,6 +42,43 @@ class EgressWeights(list):
         return (list, (list(self),))
 
 
+class EgressHandle:
+    """Stands for ``get_weights()`` where the caller only serialises it: what the mixin's
+    ``create_client_task`` / ``get_test_config`` return in place of the weights (aggregator.py:788-804,
+    806-816), which the servicer passes straight to ``serialize_response`` (:905-907).
+
+    It holds the pickled bytes of its model version (``egress_bytes``, made once per version), so
+    serialising it copies nothing and always yields the version current when it was made. Any other use
+    (indexing, iteration, ``len``, pickling) unpickles those bytes once: the same list of CPU tensors
+    ``get_weights()`` returns."""
+
+    __slots__ = ("egress_key", "egress_payload", "_weights")
+
+    def __init__(self, key, payload: bytes):
+        self.egress_key = key
+        self.egress_payload = payload
+        self._weights = None
+
+    def weights(self) -> list:
+        if self._weights is None:
+            import pickle
+
+            self._weights = pickle.loads(self.egress_payload)
+        return self._weights
+
+    def __len__(self):
+        return len(self.weights())
+
+    def __getitem__(self, i):
+        return self.weights()[i]
+
+    def __iter__(self):
+        return iter(self.weights())
+
+    def __reduce_ex__(self, protocol):
+        return (list, (list(self.weights()),))
+
+
 def _resolve_device(device) -> torch.device:
     if device is None:
         return torch.device("cuda", torch.cuda.current_device())
@@ -173,6 +210,11 @@ class TorchModelAdapter(ModelAdapterBase):
             self._egress_cache = None
             self._egress_cache = (key, pickle.dumps([t.clone() for t in self.layout.unpack(f_cpu, s_cpu)]))
         return self._egress_cache[1]
+
+    def egress_handle(self) -> EgressHandle:
+        """``get_weights()`` for a caller that only serialises it: no clone (``EgressHandle``)."""
+        key = (self._egress_id, self._version)
+        return EgressHandle(key, self.egress_bytes(key))
 
     def get_model(self):
         if self._module_version != self._version:

@@ -391,6 +391,62 @@ def test_egress_bytes_cached_per_model_version(gpu_device):
     assert pickle.loads(agg.serialize_response({"x": 1})) == {"x": 1}  # other responses: plain pickle
 
 
+def test_egress_handles_from_create_client_task(gpu_device):
+    """create_client_task / get_test_config (aggregator.py:788-816) through the mixin hand the servicer an
+    EgressHandle: serialised it is the cached bytes of its own model version (also after the model moved
+    on), used as a list it is get_weights() of that version; a plugin's own create_client_task wins."""
+    import pickle
+    import types
+
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.torch_model_adapter import EgressHandle, TorchModelAdapter
+
+    sc = Scenario("fedyogi_wide_3rounds")
+    args = sc.args()
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+
+    adapter = TorchModelAdapter(StateDictModule(sc.names, sc.init_state()),
+                                optimizer=TorchServerOptimizer(args.gradient_policy, args, "cuda:0"), device="cuda:0")
+
+    class Aggregator:  # stands for the reference class: the mixin replaces only its own methods
+        def create_client_task(self, executor_id):
+            raise AssertionError("the mixin should not call the reference create_client_task")
+
+        def get_test_config(self, client_id):
+            raise AssertionError("the mixin should not call the reference get_test_config")
+
+        def get_client_conf(self, client_id):
+            return {"learning_rate": 0.05}
+
+    class Agg(DeviceAggregator, Aggregator):
+        pass
+
+    agg = Agg(adapter, args)
+    agg.resource_manager = types.SimpleNamespace(get_next_task=lambda e: 100 + e)
+    conf, h0 = agg.create_client_task(3)
+    assert conf == {"client_id": 103, "task_config": {"learning_rate": 0.05}}
+    assert isinstance(h0, EgressHandle)
+    b0 = agg.serialize_response(h0)
+    assert b0 is h0.egress_payload and b0 is agg.serialize_response(agg.get_test_config(5)[1])
+    w0 = adapter.get_weights()
+    assert_state_equal(pickle.loads(b0), w0, "handle bytes r-init")
+    for r, ks in sc.rounds():
+        agg.start_round(len(ks))
+        for res in sc.results(ks, r):
+            agg.on_result(res)
+        h = agg.create_client_task(0)[1]
+        assert_state_equal(list(h), adapter.get_weights(), f"handle as list r{r}")
+        assert len(h) == len(w0) and torch.equal(h[0], adapter.get_weights()[0])
+    # the first handle still serialises (and reads) as the version it was made from
+    assert agg.serialize_response(h0) is b0
+    assert_state_equal(list(h0), w0, "old handle")
+    assert pickle.loads(pickle.dumps(h0)).__class__ is list  # pickles as the plain list
+    assert_state_equal(pickle.loads(pickle.dumps(h0)), w0, "old handle pickled")
+    # opt-out: the reference's fresh clone
+    agg.device_egress_handles = False
+    assert type(agg.create_client_task(1)[1]) is not EgressHandle
+
+
 @pytest.mark.parametrize("seed", [0, 1, 2])
 def test_heterofl_random_prefix_boxes_bit_exact(gpu_device, seed):
     """Random global shapes (row lengths off the 4-grid, conv kernels, 1-D and 0-d-free vectors, rows in

@@ -162,3 +162,37 @@ def test_aggregator_deserialize_hook():
     off = Plain()
     off.device_zero_copy_ingress = False
     assert off.deserialize_response(b)["update_weight"]["fc.weight"].flags.writeable
+
+
+def test_egress_handle_and_mixin_guards():
+    """EgressHandle (host-only part) and the mixin's guards: a plugin's own create_client_task /
+    get_test_config (async_aggregator.py:40, examples/auxo/aggregator.py:156,254) are left alone."""
+    import torch
+
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregatorMixin
+    from fedscale_amd.cloud.internal.torch_model_adapter import EgressHandle
+
+    ws = [torch.arange(6, dtype=torch.float32).reshape(2, 3), torch.tensor(4, dtype=torch.int64)]
+    payload = pickle.dumps(ws)
+    h = EgressHandle((1, 2), payload)
+    assert h._weights is None  # nothing unpickled until the handle is used as a list
+    assert len(h) == 2 and torch.equal(h[0], ws[0]) and torch.equal(list(h)[1], ws[1])
+    assert type(pickle.loads(pickle.dumps(h))) is list
+
+    class Plain(DeviceAggregatorMixin):
+        pass
+
+    assert Plain().serialize_response(h) is payload
+
+    class AsyncAggregator:  # a plugin with its own create_client_task
+        def create_client_task(self, executor_id):
+            return "plugin", executor_id
+
+        def get_test_config(self, client_id):
+            return "plugin-test", client_id
+
+    class Wrapped(DeviceAggregatorMixin, AsyncAggregator):
+        pass
+
+    assert Wrapped().create_client_task(7) == ("plugin", 7)
+    assert Wrapped().get_test_config(8) == ("plugin-test", 8)

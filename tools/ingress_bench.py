@@ -116,7 +116,7 @@ def egress(which, requests=8):
     rng = np.random.default_rng(1)
     upd = {n: (t.numpy() + np.float32(0.01) * rng.standard_normal(t.shape, dtype=np.float32)) if t.dtype != torch.int64
            else t.numpy() for n, t in model.state_dict().items()}
-    times = {"cached": [], "reference": []}
+    times = {"cached": [], "reference": [], "handle": [], "get_weights": []}
     for r in range(3):
         agg.start_round(2)
         agg.on_result({"client_id": 0, "update_weight": upd, "moving_loss": 1.0})
@@ -129,12 +129,22 @@ def egress(which, requests=8):
         for _ in range(requests):
             pickle.dumps(list(adapter.get_weights()))
         t2 = time.perf_counter()
+        for _ in range(requests):  # the mixin's create_client_task path (EgressHandle)
+            agg.serialize_response(adapter.egress_handle())
+        t3 = time.perf_counter()
+        for _ in range(requests):
+            adapter.get_weights()
+        t4 = time.perf_counter()
         if r > 0:
             times["cached"].append((t1 - t0) / requests)
             times["reference"].append((t2 - t1) / requests)
+            times["handle"].append((t3 - t2) / requests)
+            times["get_weights"].append((t4 - t3) / requests)
     out = {"egress": which, "requests_per_round": requests,
            "cached_ms_per_request": 1e3 * float(np.median(times["cached"])),
            "reference_pickle_ms_per_request": 1e3 * float(np.median(times["reference"])),
+           "handle_ms_per_request": 1e3 * float(np.median(times["handle"])),
+           "get_weights_clone_ms": 1e3 * float(np.median(times["get_weights"])),
            "bytes": len(agg.serialize_response(adapter.get_weights()))}
     print(json.dumps(out), flush=True)
     return out
