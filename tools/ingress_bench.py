@@ -28,12 +28,15 @@ def main():
     allout.append(run(K, rounds, which, None, loader="pickle"))
     # the mixin's deserialize_response: the same payload without copying its arrays (fedscale_amd/ingress.py)
     allout.append(run(K, rounds, which, None, loader="zerocopy"))
+    # ... with the gather + H2D of each update on a background thread (ClientStaging(async_ingress=True)):
+    # with no big copy left in deserialize_response, the main thread's next unpickle overlaps the gather
+    allout.append(run(K, rounds, which, None, loader="zerocopy", async_ingress=True))
     allout.append(egress(which))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(allout, open(os.path.join(ROOT, "gpurun_out", f"ingress_{which}_k{K}.json"), "w"), indent=1)
 
 
-def run(K, rounds, which, workers, loader=None):
+def run(K, rounds, which, workers, loader=None, async_ingress=False):
     from fedscale_amd import synth
     from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
     from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
@@ -41,11 +44,12 @@ def run(K, rounds, which, workers, loader=None):
     names, shapes, dtypes = synth.resnet18_layout() if which == "resnet18" else synth.femnist_cnn_layout()
     model = synth.LayoutModule(names, shapes, dtypes)
     adapter = TorchModelAdapter(model, device="cuda:0")
-    if workers:
+    if workers or async_ingress:
         adapter.staging = None
         from fedscale_amd.bucket import ClientStaging
 
-        adapter.staging = ClientStaging(adapter.layout, adapter.device, K, pack_workers=workers)
+        adapter.staging = ClientStaging(adapter.layout, adapter.device, K, pack_workers=workers,
+                                        async_ingress=async_ingress)
     agg = DeviceAggregator(adapter)
     rng = np.random.default_rng(0)
     pool = []
@@ -94,7 +98,7 @@ def run(K, rounds, which, workers, loader=None):
            "client_updates_per_s_incl_h2d_d2h": K / (t_round + t_egress),
            "ingress_GBps": 4 * K * P / t_round / 1e9,
            "staging_capacity": adapter.staging.capacity, "pack_workers": adapter.staging.pack_workers,
-           "from_payload": loader, "loads_ms_per_update": (t_load * 1e3 if loader else None)}
+           "from_payload": loader, "async_ingress": async_ingress, "loads_ms_per_update": (t_load * 1e3 if loader else None)}
     print(json.dumps(out), flush=True)
     return out
 
