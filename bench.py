@@ -88,6 +88,71 @@ def cpu_baseline(K: int, P: int, budget_s: float, seed: int) -> dict:
             "host": platform.processor() or platform.machine(), "host_cpus": os.cpu_count()}
 
 
+def _c1_updates(seed: int, K: int):
+    """Config 1's inputs: K FEMNIST small-CNN updates (P = 24,492) as the executor's result dicts hold
+    them (torch_client.py:76-91: numpy arrays in host memory)."""
+    import numpy as np
+
+    from fedscale_amd import synth
+
+    names, shapes, _ = synth.femnist_cnn_layout()
+    rng = np.random.default_rng(seed)
+    base = [rng.standard_normal(s, dtype=np.float32) * np.float32(0.05) for s in shapes]
+    ups = [{n: b + rng.standard_normal(b.shape, dtype=np.float32) * np.float32(0.01) for n, b in zip(names, base)}
+           for _ in range(K)]
+    return names, shapes, base, ups
+
+
+def c1_host_round(dev, seed: int, rounds: int = 50) -> dict:
+    """BASELINE config 1 (FEMNIST small-CNN, K = 10) through the drop-in: start_round, K on_result calls
+    with host dicts (pinned staging + H2D), the fused reduce, and get_weights() (D2H) — the whole round
+    the reference runs on the CPU (aggregator.py:489-511, torch_model_adapter.py:23-47)."""
+    import numpy as np
+    import torch
+
+    from fedscale_amd import synth
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    K = 10
+    names, shapes, base, ups = _c1_updates(seed, K)
+    model = synth.LayoutModule(names, shapes, [torch.float32] * len(names))
+    agg = DeviceAggregator(TorchModelAdapter(model, device=dev))
+    ts = []
+    for r in range(rounds + 5):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        agg.start_round(K)
+        for k in range(K):
+            agg.on_result({"client_id": k, "update_weight": ups[k], "moving_loss": 1.0})
+        agg.model_wrapper.get_weights()
+        ts.append(time.perf_counter() - t0)
+    ms = float(np.median(ts[5:])) * 1e3
+    return {"clients": K, "params": sum(int(np.prod(s)) for s in shapes), "round_ms_incl_h2d_d2h": ms,
+            "client_updates_per_s": K / (ms * 1e-3),
+            "note": "host dicts in, global model out (get_weights); median of %d rounds" % rounds}
+
+
+def cpu_baseline_c1(seed: int, rounds: int = 50) -> dict:
+    """The oracle's restatement of the same config-1 round on one host core (cpu_baseline leg)."""
+    import numpy as np
+
+    from oracle.cpu_reference import fedavg_close, fedavg_step
+
+    K = 10
+    _, _, _, ups = _c1_updates(seed, K)
+    ts = []
+    for r in range(rounds + 5):
+        t0 = time.perf_counter()
+        acc = None
+        for k in range(K):
+            acc = fedavg_step(acc, ups[k], k == 0)
+        fedavg_close(acc, K)
+        ts.append(time.perf_counter() - t0)
+    ms = float(np.median(ts[5:])) * 1e3
+    return {"round_ms": ms, "client_updates_per_s": K / (ms * 1e-3), "cores": 1, "kind": "port"}
+
+
 def other_configs(dev, seed: int) -> dict:
     """BASELINE.json configs 2 and 3 on one GPU (FedAvg, device-resident), beside the headline line, plus
     one GPU's shard of configs 4 and 5 (``shard_configs``).
@@ -99,7 +164,7 @@ def other_configs(dev, seed: int) -> dict:
     from fedscale_amd import synth
     from fedscale_amd.bucket import round_up
 
-    out = {}
+    out = {"c1_femnist_cnn_k10_host_round": c1_host_round(dev, seed)}
     for name, K, P, sets in (("c2_synthetic_k100_p1M", 100, 1_000_000, 2),
                              ("c3_resnet18_layout_k1000_p11191242", 1000, 11_191_242, 1)):
         ld = round_up(P, 64)
@@ -413,6 +478,8 @@ def main():
             x = None
             torch.cuda.empty_cache()
             res["cpu_baseline"] = cpu_baseline(K, P, args.cpu_seconds, args.seed)
+            if "other_configs" in res:  # the oracle on config 1's round, beside the device round
+                res["other_configs"]["c1_femnist_cnn_k10_host_round"]["cpu_baseline"] = cpu_baseline_c1(args.seed)
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)

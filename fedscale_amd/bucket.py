@@ -47,6 +47,7 @@ class Entry:
 
 
 _SUPPORTED = {torch.float32: "f", torch.int64: "i"}
+_F32, _I64 = np.dtype(np.float32), np.dtype(np.int64)
 
 
 class BucketLayout:
@@ -82,6 +83,21 @@ class BucketLayout:
         self.ldq = max(1, self.Q)
         self.f_entries = [e for e in self.entries if e.kind == "f"]
         self.i_entries = [e for e in self.entries if e.kind == "i"]
+        # static half of host_gather_plan: per entry (index, name, shape, kind, source byte offset of this
+        # rank's slice or -1 when the entry has none); destination offsets and sizes of the copied pieces
+        self._gather_entries = []
+        offs, sizes = [], []
+        for e in self.entries:
+            src = -1
+            if e.kind == "f":
+                lo, hi = max(e.offset, self.p0), min(e.offset + e.numel, self.p1)
+                if lo < hi:
+                    src = 4 * (lo - e.offset)
+                    offs.append(4 * (lo - self.p0))
+                    sizes.append(4 * (hi - lo))
+            self._gather_entries.append((e.index, e.name, e.shape, e.kind, src, e.offset))
+        self._gather_offs = np.asarray(offs, dtype=np.int64)
+        self._gather_sizes = np.asarray(sizes, dtype=np.int64)
 
     @classmethod
     def from_state_dict(cls, sd, rank: int = 0, world: int = 1) -> "BucketLayout":
@@ -109,32 +125,31 @@ class BucketLayout:
 
     def host_gather_plan(self, values: list):
         """Validate an update (shapes, dtypes) and list its byte ranges for ``run_host_gather``: the cheap,
-        synchronous half of pack_host (the caller's errors surface here, at the add, as in the reference)."""
+        synchronous half of pack_host (the caller's errors surface here, at the add, as in the reference).
+        The plan holds a reference to every source array until the copy has run."""
         values = self.values_of(values)
-        srcs, offs, sizes, keep, side = [], [], [], [], []
-        for e in self.entries:
-            v = values[e.index]
-            if isinstance(v, torch.Tensor):
-                v = v.detach().cpu().numpy()
-            a = np.asarray(v)
-            if tuple(a.shape) != e.shape:
-                raise ValueError(f"{e.name}: shape {tuple(a.shape)} != model shape {e.shape}")
-            if e.kind == "f":
-                if a.dtype != np.float32:
-                    raise TypeError(f"{e.name}: dtype {a.dtype}, the model entry is float32")
-                lo, hi = max(e.offset, self.p0), min(e.offset + e.numel, self.p1)
-                if lo < hi:
-                    flat = np.ascontiguousarray(a).reshape(-1)
-                    keep.append(flat)
-                    srcs.append(flat.ctypes.data + 4 * (lo - e.offset))
-                    offs.append(4 * (lo - self.p0))
-                    sizes.append(4 * (hi - lo))
+        ptrs, keep, side = [], [], []
+        for idx, name, shape, kind, src, off in self._gather_entries:
+            a = values[idx]
+            if type(a) is not np.ndarray:
+                if isinstance(a, torch.Tensor):
+                    a = a.detach().cpu().numpy()
+                a = np.asarray(a)
+            if a.shape != shape:
+                raise ValueError(f"{name}: shape {tuple(a.shape)} != model shape {shape}")
+            if kind == "f":
+                if a.dtype != _F32:
+                    raise TypeError(f"{name}: dtype {a.dtype}, the model entry is float32")
+                if src >= 0:
+                    if not a.flags.c_contiguous:
+                        a = np.ascontiguousarray(a)
+                    keep.append(a)
+                    ptrs.append(a.__array_interface__["data"][0] + src)
             else:
-                if a.dtype != np.int64:
-                    raise TypeError(f"{e.name}: dtype {a.dtype}, the model entry is int64")
-                side.append((e.offset, a.reshape(-1)))
-        return (np.asarray(srcs, dtype=np.uint64), np.asarray(offs, dtype=np.int64),
-                np.asarray(sizes, dtype=np.int64), keep, side)
+                if a.dtype != _I64:
+                    raise TypeError(f"{name}: dtype {a.dtype}, the model entry is int64")
+                side.append((off, a.reshape(-1)))
+        return (np.array(ptrs, dtype=np.uint64), self._gather_offs, self._gather_sizes, keep, side)
 
     def run_host_gather(self, plan, f_out: np.ndarray, i_out: np.ndarray, workers: int = 1):
         """The copying half of pack_host (no Python-level validation left; releases the GIL in C)."""
@@ -146,8 +161,10 @@ class BucketLayout:
         for off, a in side:
             i_out[off:off + a.size] = a
         if len(ps):
-            _native.call("fa_host_gather", f_out.ctypes.data, ps.ctypes.data, po.ctypes.data, pn.ctypes.data,
-                         len(ps), int(workers))
+            if len(ps) != len(po):
+                raise ValueError("pack_host: plan and layout disagree")
+            ptr = lambda a: a.__array_interface__["data"][0]  # noqa: E731 (cheaper than .ctypes.data)
+            _native.call("fa_host_gather", ptr(f_out), ptr(ps), ptr(po), ptr(pn), len(ps), int(workers))
         del keep
 
     def pack_device(self, values: list, f_dst: torch.Tensor, i_dst: torch.Tensor):
@@ -196,6 +213,7 @@ class ClientStaging:
         self.layout = layout
         self.pack_workers = pack_workers or default_pack_workers()
         self.device = torch.device(device)
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self.capacity = int(capacity)
         self.generation = 0  # bumped by every DeviceRound that takes the slots over
         self.x = torch.zeros(self.capacity, layout.ld, dtype=torch.float32, device=self.device)
@@ -204,20 +222,28 @@ class ClientStaging:
         for _ in range(ring):
             hf = torch.zeros(layout.ld, dtype=torch.float32).pin_memory()
             hi = torch.zeros(layout.ldq, dtype=torch.int64).pin_memory()
-            self._ring.append([hf, hi, None, None])  # pinned rows, event of the last H2D, pending job
+            # pinned rows, event of the last H2D, pending job, numpy views of the rows, the row's own event
+            self._ring.append([hf, hi, None, None, hf.numpy(), hi.numpy(), torch.cuda.Event()])
         self._next = 0
         self.async_ingress = async_ingress
         self._pool = None
 
-    def _copy_in(self, slot, plan, hf, hi, stream):
+    def _copy_in(self, slot, plan, r, stream, on_current: bool):
+        """Gather into ring entry r's pinned rows, then enqueue their H2D on ``stream`` and record r's event
+        (the caller has waited for that event's previous record, so re-recording it is safe)."""
         lay = self.layout
-        lay.run_host_gather(plan, hf.numpy(), hi.numpy(), workers=self.pack_workers)
-        with torch.cuda.stream(stream):
+        hf, hi, ev = r[0], r[1], r[6]
+        lay.run_host_gather(plan, r[4], r[5], workers=self.pack_workers)
+        if on_current:  # the common case: no stream switch needed
             self.x[slot, :lay.P].copy_(hf[:lay.P], non_blocking=True)
             if lay.Q:
                 self.xi[slot, :lay.Q].copy_(hi[:lay.Q], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
+        else:
+            with torch.cuda.stream(stream):
+                self.x[slot, :lay.P].copy_(hf[:lay.P], non_blocking=True)
+                if lay.Q:
+                    self.xi[slot, :lay.Q].copy_(hi[:lay.Q], non_blocking=True)
+        ev.record(stream)
         return ev
 
     def put(self, slot: int, update):
@@ -235,15 +261,15 @@ class ClientStaging:
             r[3] = None
         if r[2] is not None:
             r[2].synchronize()  # the previous H2D out of this pinned row has completed
-        stream = torch.cuda.current_stream(self.device)
+        stream = torch.cuda.current_stream(self._dev_index)
         if self.async_ingress:
             if self._pool is None:
                 from concurrent.futures import ThreadPoolExecutor
 
                 self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="fedagg-ingress")
-            r[3] = self._pool.submit(self._copy_in, slot, plan, r[0], r[1], stream)
+            r[3] = self._pool.submit(self._copy_in, slot, plan, r, stream, False)
         else:
-            r[2] = self._copy_in(slot, plan, r[0], r[1], stream)
+            r[2] = self._copy_in(slot, plan, r, stream, True)
         self._next = (self._next + 1) % len(self._ring)
 
     def drain(self):
