@@ -497,16 +497,35 @@ __device__ __forceinline__ float fast_div(float a, float b, float r) {
   const float rem = __builtin_fmaf(-q, b, a);
   return __builtin_fmaf(rem, r, q);
 }
+// QF_INFCHK 1: +-inf inputs are caught per element (max |a|).  2: they are caught once per client and
+// lane instead: an infinite a makes the fast quotient NaN (its residual is inf - inf), so the lane's
+// sum of squares is not finite and the client is redone with the IEEE division.  A finite sum that
+// overflows (|g| > 2^64) also triggers the redo, which then yields the same quotients: results never
+// depend on the choice, only the VALU count does (one op per element fewer with 2).  Measured
+// (profiles/r01_tune_qfed_infchk.log): 2 is no faster at 25 M / 12.5 M and 4 % slower at 11.19 M, so 1 stays.
+#ifndef QF_INFCHK
+#define QF_INFCHK 1
+#endif
 struct DivRange {
   int emin = 0, emax = 0;  // frexp exponents (0 for +-0): |a| in [2^(e-1), 2^e)
+#if QF_INFCHK == 1
   float amax = 0.f;        // catches +-inf (frexp reports 0 for it)
+#endif
   __device__ __forceinline__ void add(float a) {
     const int e = __builtin_amdgcn_frexp_expf(a);
     emin = e < emin ? e : emin;
     emax = e > emax ? e : emax;
+#if QF_INFCHK == 1
     amax = __builtin_fmaxf(amax, __builtin_fabsf(a));
+#endif
   }
-  __device__ __forceinline__ bool ok() const { return emin >= -79 && emax <= 80 && amax < __builtin_inff(); }
+  __device__ __forceinline__ bool ok() const {
+#if QF_INFCHK == 1
+    return emin >= -79 && emax <= 80 && amax < __builtin_inff();
+#else
+    return emin >= -79 && emax <= 80;
+#endif
+  }
 };
 
 __device__ __forceinline__ double shfl_xor_d(double v, int m) { return __shfl_xor(v, m, 64); }
@@ -604,22 +623,33 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
             rng.add(t[u][j].z);
             rng.add(t[u][j].w);
           }
-          if (!q.fast || !__all(rng.ok())) {  // rare: redo this client with the IEEE division
+          double acc = 0.0;
+#pragma unroll
+          for (int j = 0; j < QF_V; ++j) {
+            const f4 g2 = g[j] * g[j];  // torch.square(grad), fp32
+            acc += (double)((g2.x + g2.y) + (g2.z + g2.w));  // 4-term fp32 partial, then fp64
+          }
+#if QF_INFCHK == 1
+          const bool fast_ok = rng.ok();
+#else
+          const bool fast_ok = rng.ok() && __builtin_isfinite(acc);
+#endif
+          if (!q.fast || !__all(fast_ok)) {  // rare: redo this client with the IEEE division
+            acc = 0.0;
 #pragma unroll
             for (int j = 0; j < QF_V; ++j) {
               g[j].x = __fdiv_rn(t[u][j].x, q.lr);
               g[j].y = __fdiv_rn(t[u][j].y, q.lr);
               g[j].z = __fdiv_rn(t[u][j].z, q.lr);
               g[j].w = __fdiv_rn(t[u][j].w, q.lr);
+              const f4 g2 = g[j] * g[j];
+              acc += (double)((g2.x + g2.y) + (g2.z + g2.w));
             }
           }
-          double acc = 0.0;
 #pragma unroll
           for (int j = 0; j < QF_V; ++j) {
             const f4 term = al * g[j];  // optimizers.py:89,93  float_power(...) * grad (fp32 product)
             D[j] = first ? term : D[j] + term;
-            const f4 g2 = g[j] * g[j];  // torch.square(grad), fp32
-            acc += (double)((g2.x + g2.y) + (g2.z + g2.w));  // 4-term fp32 partial, then fp64
           }
           v[u0 + u] = acc;
         }

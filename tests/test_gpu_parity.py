@@ -326,6 +326,46 @@ def test_qfed_division_is_correctly_rounded(gpu_device, lr):
     assert (np.signbit(got) == np.signbit(want))[~np.isnan(want)].all()
 
 
+@pytest.mark.parametrize("lr", [0.05, 3e-6, 7.5e5])
+def test_qfed_inf_and_overflow_in_otherwise_fast_waves(gpu_device, lr):
+    """Waves whose values are all in the fast-division range except a lone +-inf / NaN, or whose squares
+    overflow fp32: the per-client finiteness check (QF_INFCHK 2) must send them to the IEEE division.
+    Two clients, so the fallback of one client does not leak into the other's delta or norm."""
+    from fedscale_amd import kernels as kx
+
+    rng = np.random.default_rng(11)
+    n = 1 << 20
+    K = 2
+    a = (rng.uniform(1.0, 2.0, size=(K, n)) * np.exp2(rng.integers(-40, 40, size=(K, n)).astype(np.float64)))
+    a = a.astype(np.float32)
+    a[rng.random((K, n)) < 0.5] *= -1
+    for pos in rng.choice(n, size=24, replace=False):  # lone specials in different waves
+        a[0, pos] = rng.choice([np.inf, -np.inf, np.nan])
+    big = rng.choice(n, size=24, replace=False)  # |g| beyond 2^64: g*g overflows, the value stays finite
+    a[1, big] = np.float32(2.0 ** 79) * np.float32(1.5)
+    x = torch.from_numpy(-a).cuda()
+    last = torch.zeros(n, device="cuda")
+    delta = torch.empty(n, device="cuda")
+    sq = torch.zeros(K, dtype=torch.float64, device="cuda")
+    alpha = torch.tensor([1.0, 0.5], device="cuda")
+    with np.errstate(all="ignore"):
+        g = (np.float32(0) - (-a)) / np.float32(lr)
+        want = g[0] * np.float32(1.0)
+        want = want + g[1] * np.float32(0.5)
+    kx.qfed_accumulate(x, K, n, last=last, alpha=alpha, lr=lr, delta=delta, sqnorm=sq,
+                       workspace=kx.qfed_workspace(K, "cuda"), accumulate=False)
+    got = delta.cpu().numpy()
+    same = (got == want) | (np.isnan(got) & np.isnan(want))
+    assert same.all(), f"{(~same).sum()} mismatches, e.g. got={got[~same][:3]} want={want[~same][:3]}"
+    s = sq.cpu().numpy()
+    assert np.isnan(s[0]) or np.isinf(s[0])
+    with np.errstate(all="ignore"):
+        ref1 = np.sum(np.square(g[1]).astype(np.float64))
+    assert np.isinf(s[1]) == np.isinf(ref1)
+    if not np.isinf(ref1):
+        assert abs(s[1] - ref1) <= 1e-9 * ref1
+
+
 @pytest.mark.parametrize("capacity", [None, 2])
 @pytest.mark.parametrize("name", scenario_names("cohorts"))
 def test_auxo_cohorts_match_reference_fixture(gpu_device, name, capacity):

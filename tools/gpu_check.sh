@@ -88,7 +88,7 @@ if [[ $STAGE == policies ]]; then
 fi
 if [[ $STAGE == tuneqf ]]; then
   for P in ${QFP:-25000000}; do
-    timeout -k 10 600 python tools/tune_qfed.py ${QFK:-1000} $P 3 > $OUT/tune_qf_$P.log 2>&1 || { tail -20 $OUT/tune_qf_$P.log; exit 1; }
+    timeout -k 10 600 python tools/tune_qfed.py ${QFK:-1000} $P ${QFR:-3} > $OUT/tune_qf_$P.log 2>&1 || { tail -20 $OUT/tune_qf_$P.log; exit 1; }
     cat $OUT/tune_qf_$P.log
   done
 fi
