@@ -131,6 +131,9 @@ struct RedArgs {
 
 // V: float4 per lane per client (a wave covers V KiB contiguous of one client row)
 // U: clients loaded ahead of the adds
+#ifndef FA_XCD_REMAP
+#define FA_XCD_REMAP 0  // 1: capped-grid workgroups of one XCD take adjacent tiles (tuning experiment)
+#endif
 #ifndef FA_RED_WAVES
 #define FA_RED_WAVES 4
 #endif
@@ -227,7 +230,16 @@ __global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   if (LOOP) {
-    for (int64_t tile = blockIdx.x; tile < r.ntiles; tile += gridDim.x) reduce_tile<V, U, EPI, W>(r, tile, lane, wave);
+    int64_t b = blockIdx.x;
+#if FA_XCD_REMAP
+    // workgroups are dispatched round-robin over the 8 XCDs (b -> XCD b % 8): give each XCD a contiguous
+    // run of the grid's concurrent tiles instead of every 8th one (bijective for any grid size)
+    {
+      const int64_t G = gridDim.x, q = G / 8, rem = G % 8, x = b % 8;
+      b = x * q + (x < rem ? x : rem) + b / 8;
+    }
+#endif
+    for (int64_t tile = b; tile < r.ntiles; tile += gridDim.x) reduce_tile<V, U, EPI, W>(r, tile, lane, wave);
   } else {
     reduce_tile<V, U, EPI, W>(r, blockIdx.x, lane, wave);
   }

@@ -61,7 +61,7 @@ if [[ $STAGE == tune ]]; then
   cat $OUT/tune_c2.log
 fi
 if [[ $STAGE == sweep ]]; then
-  timeout -k 10 1000 python tools/tune_reduce.py sweep ${SWEEP:-1000:25000000,1000:11191242,1000:12500000,400:50000000,1000:4000000,100:1000000} 3 > $OUT/sweep.log 2>&1 || { tail -20 $OUT/sweep.log; exit 1; }
+  timeout -k 10 1000 python tools/tune_reduce.py sweep ${SWEEP:-1000:25000000,1000:11191242,1000:12500000,400:50000000,1000:4000000,100:1000000} ${SWR:-3} > $OUT/sweep.log 2>&1 || { tail -20 $OUT/sweep.log; exit 1; }
   cat $OUT/sweep.log
 fi
 if [[ $STAGE == dist ]]; then
