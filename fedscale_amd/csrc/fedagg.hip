@@ -562,6 +562,9 @@ __device__ __forceinline__ f4 rows_load(__amdgpu_buffer_rsrc_t r, uint32_t voff)
 #ifndef QF_MINW
 #define QF_MINW 1
 #endif
+#ifndef QF_PIPE
+#define QF_PIPE 0  // 1: software-pipelined client loads (two row buffers)
+#endif
 // WIDE: one descriptor spans all QF_G rows of a group (QF_G rows < 4 GiB); otherwise one per QF_U rows.
 template <bool WIDE>
 __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
@@ -593,13 +596,98 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       D[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.delta)[c0 + 64 * j]
                                                   : f4{0.f, 0.f, 0.f, 0.f};
     }
+    // one client: g = (L - W)/lr from its loaded row slice t (overwritten with L - W), delta chain and the
+    // lane's fp64 sum of squares
+    auto client = [&](f4(&t)[QF_V], int kk, float al) -> double {
+      const bool first = (kk == 0) && !(q.flags & FA_ACCUMULATE);
+      f4 g[QF_V];
+      DivRange rng;
+#pragma unroll
+      for (int j = 0; j < QF_V; ++j) {
+        t[j] = L[j] - t[j];  // (last - W), optimizers.py:83; the "* 1.0" is exact
+        g[j].x = fast_div(t[j].x, q.lr, q.rlr);
+        g[j].y = fast_div(t[j].y, q.lr, q.rlr);
+        g[j].z = fast_div(t[j].z, q.lr, q.rlr);
+        g[j].w = fast_div(t[j].w, q.lr, q.rlr);
+        rng.add(t[j].x);
+        rng.add(t[j].y);
+        rng.add(t[j].z);
+        rng.add(t[j].w);
+      }
+      double acc = 0.0;
+#pragma unroll
+      for (int j = 0; j < QF_V; ++j) {
+        const f4 g2 = g[j] * g[j];  // torch.square(grad), fp32
+        acc += (double)((g2.x + g2.y) + (g2.z + g2.w));  // 4-term fp32 partial, then fp64
+      }
+#if QF_INFCHK == 1
+      const bool fast_ok = rng.ok();
+#else
+      const bool fast_ok = rng.ok() && __builtin_isfinite(acc);
+#endif
+      if (!q.fast || !__all(fast_ok)) {  // rare: redo this client with the IEEE division
+        acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < QF_V; ++j) {
+          g[j].x = __fdiv_rn(t[j].x, q.lr);
+          g[j].y = __fdiv_rn(t[j].y, q.lr);
+          g[j].z = __fdiv_rn(t[j].z, q.lr);
+          g[j].w = __fdiv_rn(t[j].w, q.lr);
+          const f4 g2 = g[j] * g[j];
+          acc += (double)((g2.x + g2.y) + (g2.z + g2.w));
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < QF_V; ++j) {
+        const f4 term = al * g[j];  // optimizers.py:89,93  float_power(...) * grad (fp32 product)
+        D[j] = first ? term : D[j] + term;
+      }
+      return acc;
+    };
+#if QF_PIPE
+    // software pipeline: client k+1's row slice is requested before client k is computed, so a wave's
+    // loads stay in flight through its ~800 VALU ops per client (two row buffers in registers)
+    // Branch-free: a client k >= K gets an empty range (the loads return zeros and touch no memory), so
+    // the waitcnt pass sees the same loads in flight on every path and never falls back to vmcnt(0).
+    auto issue = [&](f4(&dst)[QF_V], float& al, int k) {
+      // the client's alpha travels with its rows: a load issued later would make the wait for it a
+      // wait for every load in flight (the vector memory counter retires in order)
+      al = q.alpha[k < q.K ? k : q.K - 1];
+      if (WIDE) {
+        const int kg = k & ~(QF_G - 1);
+        const int nr = q.K - kg;
+        const int nrows = nr < 0 ? 0 : (nr < QF_G ? nr : QF_G);
+        const __amdgpu_buffer_rsrc_t grp = rows_rsrc(q.x + (int64_t)kg * q.ld4 * 4, (uint32_t)nrows * rowbytes);
+        const uint32_t roff = (uint32_t)(k - kg) * rowbytes;
+#pragma unroll
+        for (int j = 0; j < QF_V; ++j) dst[j] = rows_load(grp, voff[j] + roff);
+      } else {
+        const __amdgpu_buffer_rsrc_t rr =
+            rows_rsrc(q.x + (int64_t)k * q.ld4 * 4, k < q.K ? (uint32_t)(q.P4 * 16) : 0u);
+#pragma unroll
+        for (int j = 0; j < QF_V; ++j) dst[j] = rows_load(rr, voff[j]);
+      }
+    };
+    f4 pb[2][QF_V];
+    float pa[2];
+    issue(pb[0], pa[0], 0);
+#endif
     for (int kg = 0; kg < q.K; kg += QF_G) {
-      const int nrows = q.K - kg < QF_G ? q.K - kg : QF_G;
-      const float* row0 = q.x + (int64_t)kg * q.ld4 * 4;
-      const __amdgpu_buffer_rsrc_t grp = rows_rsrc(row0, WIDE ? (uint32_t)nrows * rowbytes : 0u);
       double v[QF_G];
 #pragma unroll
       for (int jj = 0; jj < QF_G; ++jj) v[jj] = 0.0;
+#if QF_PIPE
+      static_assert(QF_G % 2 == 0, "the two row buffers alternate within a group");
+#pragma unroll
+      for (int u = 0; u < QF_G; ++u) {
+        const int kk = kg + u;
+        issue(pb[(u + 1) & 1], pa[(u + 1) & 1], kk + 1);  // past K: an empty range (see issue)
+        if (kk < q.K) v[u] = client(pb[u & 1], kk, pa[u & 1]);
+      }
+#else
+      const int nrows = q.K - kg < QF_G ? q.K - kg : QF_G;
+      const float* row0 = q.x + (int64_t)kg * q.ld4 * 4;
+      const __amdgpu_buffer_rsrc_t grp = rows_rsrc(row0, WIDE ? (uint32_t)nrows * rowbytes : 0u);
 #pragma unroll
       for (int u0 = 0; u0 < QF_G; u0 += QF_U) {
         f4 t[QF_U][QF_V];
@@ -619,53 +707,10 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
         for (int u = 0; u < QF_U; ++u) {
           const int kk = kg + u0 + u;
           if (kk >= q.K) break;  // uniform
-          const float al = q.alpha[kk];
-          const bool first = (kk == 0) && !(q.flags & FA_ACCUMULATE);
-          f4 g[QF_V];
-          DivRange rng;
-#pragma unroll
-          for (int j = 0; j < QF_V; ++j) {
-            t[u][j] = L[j] - t[u][j];  // (last - W), optimizers.py:83; the "* 1.0" is exact
-            g[j].x = fast_div(t[u][j].x, q.lr, q.rlr);
-            g[j].y = fast_div(t[u][j].y, q.lr, q.rlr);
-            g[j].z = fast_div(t[u][j].z, q.lr, q.rlr);
-            g[j].w = fast_div(t[u][j].w, q.lr, q.rlr);
-            rng.add(t[u][j].x);
-            rng.add(t[u][j].y);
-            rng.add(t[u][j].z);
-            rng.add(t[u][j].w);
-          }
-          double acc = 0.0;
-#pragma unroll
-          for (int j = 0; j < QF_V; ++j) {
-            const f4 g2 = g[j] * g[j];  // torch.square(grad), fp32
-            acc += (double)((g2.x + g2.y) + (g2.z + g2.w));  // 4-term fp32 partial, then fp64
-          }
-#if QF_INFCHK == 1
-          const bool fast_ok = rng.ok();
-#else
-          const bool fast_ok = rng.ok() && __builtin_isfinite(acc);
-#endif
-          if (!q.fast || !__all(fast_ok)) {  // rare: redo this client with the IEEE division
-            acc = 0.0;
-#pragma unroll
-            for (int j = 0; j < QF_V; ++j) {
-              g[j].x = __fdiv_rn(t[u][j].x, q.lr);
-              g[j].y = __fdiv_rn(t[u][j].y, q.lr);
-              g[j].z = __fdiv_rn(t[u][j].z, q.lr);
-              g[j].w = __fdiv_rn(t[u][j].w, q.lr);
-              const f4 g2 = g[j] * g[j];
-              acc += (double)((g2.x + g2.y) + (g2.z + g2.w));
-            }
-          }
-#pragma unroll
-          for (int j = 0; j < QF_V; ++j) {
-            const f4 term = al * g[j];  // optimizers.py:89,93  float_power(...) * grad (fp32 product)
-            D[j] = first ? term : D[j] + term;
-          }
-          v[u0 + u] = acc;
+          v[u0 + u] = client(t[u], kk, q.alpha[kk]);
         }
       }
+#endif
       // multi-reduce: QF_G values per lane -> lane l holds the wave sum of client (l >> s) & (QF_G-1)
       double y;
       const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
