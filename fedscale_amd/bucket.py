@@ -208,8 +208,13 @@ class ClientStaging:
     the slots.
     """
 
+    #: staging areas of at most this many bytes take the bulk path: every update is gathered into a
+    #: pinned mirror of the whole area and one H2D per drain() moves all pending rows (small models pay
+    #: the per-update copy-enqueue latency otherwise; DESIGN.md §5, config 1)
+    BULK_MAX_BYTES = 64 << 20
+
     def __init__(self, layout: BucketLayout, device, capacity: int, ring: int = 2,
-                 pack_workers: Optional[int] = None, async_ingress: bool = False):
+                 pack_workers: Optional[int] = None, async_ingress: bool = False, bulk: Optional[bool] = None):
         self.layout = layout
         self.pack_workers = pack_workers or default_pack_workers()
         self.device = torch.device(device)
@@ -227,6 +232,17 @@ class ClientStaging:
         self._next = 0
         self.async_ingress = async_ingress
         self._pool = None
+        nbytes = self.capacity * (layout.ld * 4 + layout.ldq * 8)
+        self.bulk = (not async_ingress and nbytes <= self.BULK_MAX_BYTES) if bulk is None else bool(bulk)
+        if self.bulk and async_ingress:
+            raise ValueError("bulk staging and async_ingress are exclusive")
+        if self.bulk:
+            self._hx = torch.zeros(self.capacity, layout.ld, dtype=torch.float32).pin_memory()
+            self._hxi = torch.zeros(self.capacity, layout.ldq, dtype=torch.int64).pin_memory()
+            self._hx_np, self._hxi_np = self._hx.numpy(), self._hxi.numpy()
+            self._bulk_lo = self._bulk_hi = 0  # host rows [lo, hi) not yet copied to the device
+            self._bulk_ev = torch.cuda.Event()
+            self._bulk_busy = False  # an H2D out of the mirror may still be running
 
     def _copy_in(self, slot, plan, r, stream, on_current: bool):
         """Gather into ring entry r's pinned rows, then enqueue their H2D on ``stream`` and record r's event
@@ -255,6 +271,9 @@ class ClientStaging:
             lay.pack_device(values, self.x[slot], self.xi[slot])
             return
         plan = lay.host_gather_plan(values)  # validation errors surface here, synchronously
+        if self.bulk:
+            self._put_bulk(slot, plan)
+            return
         r = self._ring[self._next]
         if r[3] is not None:  # the job that last used this pinned row
             r[2] = r[3].result()
@@ -272,8 +291,34 @@ class ClientStaging:
             r[2] = self._copy_in(slot, plan, r, stream, True)
         self._next = (self._next + 1) % len(self._ring)
 
+    def _put_bulk(self, slot: int, plan):
+        lay = self.layout
+        if self._bulk_busy:  # the mirror's previous H2D must finish before its rows are rewritten
+            self._bulk_ev.synchronize()
+            self._bulk_busy = False
+        if self._bulk_hi > self._bulk_lo and slot != self._bulk_hi:
+            self.drain()  # keep pending rows contiguous
+        if self._bulk_hi == self._bulk_lo:
+            self._bulk_lo = self._bulk_hi = slot
+        lay.run_host_gather(plan, self._hx_np[slot], self._hxi_np[slot], workers=self.pack_workers)
+        self._bulk_hi = slot + 1
+
+    def _drain_bulk(self):
+        lo, hi = self._bulk_lo, self._bulk_hi
+        if hi > lo:
+            # whole rows: one contiguous block (the mirror's padding columns are zero, as on the device)
+            self.x[lo:hi].copy_(self._hx[lo:hi], non_blocking=True)
+            if self.layout.Q:
+                self.xi[lo:hi].copy_(self._hxi[lo:hi], non_blocking=True)
+            self._bulk_ev.record(torch.cuda.current_stream(self._dev_index))
+            self._bulk_busy = True
+            self._bulk_lo = self._bulk_hi = 0
+
     def drain(self):
         """Wait until every queued copy has been enqueued on its stream (re-raising a copy's error)."""
+        if self.bulk:
+            self._drain_bulk()
+            return
         for r in self._ring:
             if r[3] is not None:
                 r[2] = r[3].result()

@@ -50,9 +50,15 @@ def _device_run(sc, capacity=None):
         yield r, adapter, opt, agg
 
 
+@pytest.mark.parametrize("bulk", [True, False], ids=["bulk", "perupdate"])
 @pytest.mark.parametrize("capacity", [None, 2])
 @pytest.mark.parametrize("name", scenario_names())
-def test_device_path_matches_reference_fixture(gpu_device, name, capacity):
+def test_device_path_matches_reference_fixture(gpu_device, name, capacity, bulk, monkeypatch):
+    """Every fixture through the device path, with the small-model bulk staging (one H2D per drain) and
+    with the per-update H2D ring that large models use."""
+    from fedscale_amd.bucket import ClientStaging
+
+    monkeypatch.setattr(ClientStaging, "BULK_MAX_BYTES", ClientStaging.BULK_MAX_BYTES if bulk else -1)
     sc = Scenario(name)
     for r, adapter, opt, agg in _device_run(sc, capacity):
         got = adapter.get_weights()
