@@ -205,7 +205,8 @@ class ClientStaging:
     measured with the executor's pickled payloads, the background copy and the main thread's
     ``pickle.loads`` (aggregator.py:704) serialise on the GIL and halve the rate.
     ``drain()`` waits for every queued copy to be enqueued; DeviceRound calls it before any kernel reads
-    the slots.
+    the slots.  Small staging areas (``bulk``, <= BULK_MAX_BYTES) skip the per-update H2D: updates are
+    gathered into a pinned mirror of the whole area and ``drain()`` moves the pending rows in one copy.
     """
 
     #: staging areas of at most this many bytes take the bulk path: every update is gathered into a
