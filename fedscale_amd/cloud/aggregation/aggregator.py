@@ -36,6 +36,9 @@ class DeviceAggregatorMixin:
     #: create_client_task / get_test_config hand the servicer an EgressHandle (the cached pickled bytes of
     #: the model version) instead of a fresh clone of the model per request
     device_egress_handles = True
+    #: pickled bytes kept for past model versions' get_weights() lists (FedBuff's model_cache holds
+    #: max_staleness + 1 of them, config_parser.py:123)
+    device_egress_past_versions = 8
 
     _device_round = None
 
@@ -97,7 +100,19 @@ class DeviceAggregatorMixin:
                 b = w.egress_bytes(key) if isinstance(w, TorchModelAdapter) else None
                 if b is not None:
                     return b
-            responses = list(responses)
+            # a past model version: FedBuff hands out the lists of its model_cache
+            # (async_aggregator.py:54,71-73) again for every client task; each list object pickles once
+            import pickle
+
+            old = self.__dict__.setdefault("_egress_past", {})
+            hit = old.get(id(responses))
+            if hit is not None and hit[0] is responses:
+                return hit[1]
+            b = pickle.dumps(list(responses))
+            if len(old) >= self.device_egress_past_versions:
+                old.pop(next(iter(old)))
+            old[id(responses)] = (responses, b)  # holds the list, so its id stays unique
+            return b
         sup = getattr(super(), "serialize_response", None)
         if sup is not None:
             return sup(responses)

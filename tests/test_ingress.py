@@ -196,3 +196,31 @@ def test_egress_handle_and_mixin_guards():
 
     assert Wrapped().create_client_task(7) == ("plugin", 7)
     assert Wrapped().get_test_config(8) == ("plugin-test", 8)
+
+
+def test_egress_bytes_of_past_versions_cached_per_list():
+    """FedBuff's create_client_task hands out the model_cache lists of past versions
+    (async_aggregator.py:54): each list object is pickled once, and the bytes are pickle.dumps of it."""
+    import torch
+
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregatorMixin
+    from fedscale_amd.cloud.internal.torch_model_adapter import EgressWeights
+
+    class Plain(DeviceAggregatorMixin):
+        model_wrapper = None
+
+    agg = Plain()
+    lists = []
+    for v in range(10):
+        w = EgressWeights([torch.full((3, 2), float(v)), torch.tensor(v, dtype=torch.int64)])
+        w.egress_key = (12345, v)  # no adapter of this aggregator holds these versions
+        lists.append(w)
+    b0 = agg.serialize_response(lists[0])
+    assert agg.serialize_response(lists[0]) is b0
+    assert b0 == pickle.dumps([lists[0][0], lists[0][1]])
+    assert type(pickle.loads(b0)) is list
+    for w in lists[1:]:
+        agg.serialize_response(w)
+    assert len(agg._egress_past) == agg.device_egress_past_versions
+    b0_again = agg.serialize_response(lists[0])  # evicted: pickled again, same bytes
+    assert b0_again == b0 and b0_again is not b0
