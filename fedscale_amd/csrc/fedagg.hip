@@ -563,7 +563,7 @@ __device__ __forceinline__ f4 rows_load(__amdgpu_buffer_rsrc_t r, uint32_t voff)
 #define QF_MINW 1
 #endif
 #ifndef QF_PIPE
-#define QF_PIPE 0  // 1: software-pipelined client loads (two row buffers)
+#define QF_PIPE 0  // 1: software-pipelined client loads (two row buffers); measured slower, see DESIGN.md
 #endif
 // WIDE: one descriptor spans all QF_G rows of a group (QF_G rows < 4 GiB); otherwise one per QF_U rows.
 template <bool WIDE>
@@ -596,6 +596,23 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       D[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.delta)[c0 + 64 * j]
                                                   : f4{0.f, 0.f, 0.f, 0.f};
     }
+    // row slice of client k (k >= K: an empty range, the loads return zeros and touch no memory)
+    auto load_rows = [&](f4(&dst)[QF_V], int k) {
+      if (WIDE) {
+        const int kg = k & ~(QF_G - 1);
+        const int nr = q.K - kg;
+        const int nrows = nr < 0 ? 0 : (nr < QF_G ? nr : QF_G);
+        const __amdgpu_buffer_rsrc_t grp = rows_rsrc(q.x + (int64_t)kg * q.ld4 * 4, (uint32_t)nrows * rowbytes);
+        const uint32_t roff = (uint32_t)(k - kg) * rowbytes;
+#pragma unroll
+        for (int j = 0; j < QF_V; ++j) dst[j] = rows_load(grp, voff[j] + roff);
+      } else {
+        const __amdgpu_buffer_rsrc_t rr =
+            rows_rsrc(q.x + (int64_t)k * q.ld4 * 4, k < q.K ? (uint32_t)(q.P4 * 16) : 0u);
+#pragma unroll
+        for (int j = 0; j < QF_V; ++j) dst[j] = rows_load(rr, voff[j]);
+      }
+    };
     // one client: g = (L - W)/lr from its loaded row slice t (overwritten with L - W), delta chain and the
     // lane's fp64 sum of squares
     auto client = [&](f4(&t)[QF_V], int kk, float al) -> double {
@@ -653,20 +670,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       // the client's alpha travels with its rows: a load issued later would make the wait for it a
       // wait for every load in flight (the vector memory counter retires in order)
       al = q.alpha[k < q.K ? k : q.K - 1];
-      if (WIDE) {
-        const int kg = k & ~(QF_G - 1);
-        const int nr = q.K - kg;
-        const int nrows = nr < 0 ? 0 : (nr < QF_G ? nr : QF_G);
-        const __amdgpu_buffer_rsrc_t grp = rows_rsrc(q.x + (int64_t)kg * q.ld4 * 4, (uint32_t)nrows * rowbytes);
-        const uint32_t roff = (uint32_t)(k - kg) * rowbytes;
-#pragma unroll
-        for (int j = 0; j < QF_V; ++j) dst[j] = rows_load(grp, voff[j] + roff);
-      } else {
-        const __amdgpu_buffer_rsrc_t rr =
-            rows_rsrc(q.x + (int64_t)k * q.ld4 * 4, k < q.K ? (uint32_t)(q.P4 * 16) : 0u);
-#pragma unroll
-        for (int j = 0; j < QF_V; ++j) dst[j] = rows_load(rr, voff[j]);
-      }
+      load_rows(dst, k);
     };
     f4 pb[2][QF_V];
     float pa[2];
