@@ -224,3 +224,20 @@ def test_egress_bytes_of_past_versions_cached_per_list():
     assert len(agg._egress_past) == agg.device_egress_past_versions
     b0_again = agg.serialize_response(lists[0])  # evicted: pickled again, same bytes
     assert b0_again == b0 and b0_again is not b0
+
+
+def test_torch_state_dict_payload_falls_back():
+    """HeteroFL clients upload a torch state_dict (examples/heterofl/customized_client.py:93): tensors
+    pickle through torch's own reducers, which the fast path does not rebuild; the result is still
+    exactly pickle.loads'."""
+    from collections import OrderedDict
+
+    import torch
+
+    sd = OrderedDict(w=torch.arange(5000, dtype=torch.float32).reshape(50, 100), n=torch.tensor(3))
+    b = pickle.dumps({"client_id": 1, "local_parameters": sd, "update_weight": {"x": np.ones(4096, np.float32)}})
+    got, ref = ingress.loads(b), pickle.loads(b)
+    assert type(got["local_parameters"]) is OrderedDict
+    for k in sd:
+        assert torch.equal(got["local_parameters"][k], ref["local_parameters"][k])
+    assert np.array_equal(got["update_weight"]["x"], ref["update_weight"]["x"])
