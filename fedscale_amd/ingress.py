@@ -36,6 +36,11 @@ from . import _native
 #: own rebuild (C) is cheaper than a view built in Python (measured on a ResNet-18 payload)
 MIN_BYTES = 4096
 
+#: payloads smaller than this go straight to pickle.loads: below about a MiB its single copy costs less
+#: than the strip + placeholder pass (measured: 98 KB FEMNIST update 25 us vs 92 us; 45 MB ResNet-18
+#: update 39 ms vs 1 ms on this container's host)
+MIN_PAYLOAD = 1 << 20
+
 _TAG = b"FAPB"
 _RECONSTRUCT = {("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct")}
 
@@ -165,10 +170,12 @@ def strip(payload: bytes, min_bytes: int = MIN_BYTES):
     return ctypes.string_at(out, n), [(regions[2 * i], regions[2 * i + 1]) for i in range(r)]
 
 
-def loads(payload, min_bytes: int | None = None):
+def loads(payload, min_bytes: int | None = None, min_payload: int | None = None):
     """``pickle.loads(payload)`` without copying the large byte strings (module docstring)."""
     min_bytes = MIN_BYTES if min_bytes is None else int(min_bytes)
-    if type(payload) is not bytes or len(payload) < 2 * min_bytes or payload[:2] != b"\x80\x04":
+    min_payload = MIN_PAYLOAD if min_payload is None else int(min_payload)
+    if (type(payload) is not bytes or len(payload) < max(2 * min_bytes, min_payload)
+            or payload[:2] != b"\x80\x04"):
         return pickle.loads(payload)
     try:
         stream, regions = strip(payload, min_bytes)

@@ -171,6 +171,7 @@ def test_zero_copy_payload_ingress_matches_reference(gpu_device, name, monkeypat
     from tests.golden_io import Scenario, StateDictModule, assert_state_close, assert_state_equal
 
     monkeypatch.setattr(ingress, "MIN_BYTES", 256)  # strip every array that pickles as BINBYTES (>= 256 B)
+    monkeypatch.setattr(ingress, "MIN_PAYLOAD", 0)  # the fixtures' payloads are small
     sc = Scenario(name)
     args = sc.args()
     opt = TorchServerOptimizer(args.gradient_policy, args, "cuda:0") if sc.meta.get("optimizer") else None

@@ -10,6 +10,12 @@ import pytest
 from fedscale_amd import _native, ingress
 
 
+@pytest.fixture(autouse=True)
+def _fast_path_for_small_payloads(monkeypatch):
+    """The cases here are small; exercise the zero-copy path on them (production: >= MIN_PAYLOAD)."""
+    monkeypatch.setattr(ingress, "MIN_PAYLOAD", 0)
+
+
 def _assert_same(a, b, path="root"):
     assert type(a) is type(b), path
     if isinstance(a, np.ndarray):
@@ -241,3 +247,16 @@ def test_torch_state_dict_payload_falls_back():
     for k in sd:
         assert torch.equal(got["local_parameters"][k], ref["local_parameters"][k])
     assert np.array_equal(got["update_weight"]["x"], ref["update_weight"]["x"])
+
+
+def test_small_payloads_take_pickle_loads(monkeypatch):
+    """Below MIN_PAYLOAD the fast path costs more than pickle's copy: plain pickle.loads (writable arrays)."""
+    monkeypatch.setattr(ingress, "MIN_PAYLOAD", 1 << 20)
+    b = pickle.dumps(_executor_result())
+    assert len(b) < 1 << 20
+    got = ingress.loads(b)
+    assert got["update_weight"]["fc.weight"].flags.writeable
+    _assert_same(got, pickle.loads(b))
+    big = pickle.dumps(_executor_result(scale=64))
+    assert len(big) >= 1 << 20
+    assert not ingress.loads(big)["update_weight"]["fc.weight"].flags.writeable
