@@ -150,6 +150,19 @@ class DeviceAggregatorMixin:
             return super().get_test_config(client_id)
         return {"client_id": client_id}, self._egress_weights()
 
+    def CLIENT_PING(self, request, context):
+        """aggregator.py:870-912, the reference servicer itself. Its UPDATE_MODEL branch (:902-903) calls
+        ``model_wrapper.get_weights()`` only to serialise it (:905-907), so for that one call the adapter
+        hands back an EgressHandle on the cached bytes instead of cloning the model."""
+        sup = super().CLIENT_PING
+        w = self.model_wrapper
+        q = getattr(self, "individual_client_events", {}).get(request.executor_id)
+        if (self.device_egress_handles and isinstance(w, TorchModelAdapter) and q
+                and q[0] == "update_model" and self._reference_impl("CLIENT_PING")):  # commons.UPDATE_MODEL
+            with w.handle_next_get_weights():
+                return sup(request, context)
+        return sup(request, context)
+
     def update_weight_aggregation(self, results):
         w = self._wrapper()
         if self._is_first_result_in_round() or self._device_round is None:

@@ -18,6 +18,7 @@ Device fast path used by ``DeviceAggregatorMixin``:
 from __future__ import annotations
 
 import itertools
+import threading
 from typing import List, Optional
 
 import numpy as np
@@ -30,6 +31,9 @@ from .model_adapter_base import ModelAdapterBase
 
 
 _EGRESS_IDS = itertools.count(1)
+#: per servicer thread: the adapter whose next get_weights() call hands out an EgressHandle
+#: (set by the aggregator mixin around the reference CLIENT_PING's UPDATE_MODEL branch)
+_HANDLE_ONCE = threading.local()
 
 
 class EgressWeights(list):
@@ -189,9 +193,13 @@ class TorchModelAdapter(ModelAdapterBase):
 
     def get_weights(self) -> List[torch.Tensor]:
         """torch_model_adapter.py:41-47: cloned CPU tensors in state_dict order (gathers the shards).
+        Inside ``handle_next_get_weights`` (this thread only) the one next call returns an EgressHandle.
 
         The list is tagged with (adapter, model version) so that the aggregator's serialize_response can
         hand out the pickled bytes of this version, made once per round (``egress_bytes``)."""
+        if getattr(_HANDLE_ONCE, "adapter", None) is self:  # the caller only serialises this list
+            _HANDLE_ONCE.adapter = None
+            return self.egress_handle()
         f_cpu, s_cpu = self._host_copy()
         out = EgressWeights(t.clone() for t in self.layout.unpack(f_cpu, s_cpu))
         out.egress_key = (self._egress_id, self._version)
@@ -215,6 +223,22 @@ class TorchModelAdapter(ModelAdapterBase):
         """``get_weights()`` for a caller that only serialises it: no clone (``EgressHandle``)."""
         key = (self._egress_id, self._version)
         return EgressHandle(key, self.egress_bytes(key))
+
+    def handle_next_get_weights(self):
+        """Context: the next get_weights() on this thread returns ``egress_handle()`` (no clone). For a
+        caller that only serialises the list, such as the servicer's UPDATE_MODEL branch
+        (aggregator.py:902-907)."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def ctx():
+            _HANDLE_ONCE.adapter = self
+            try:
+                yield
+            finally:
+                _HANDLE_ONCE.adapter = None
+
+        return ctx()
 
     def get_model(self):
         if self._module_version != self._version:

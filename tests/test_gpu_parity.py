@@ -464,11 +464,17 @@ def test_egress_handles_from_create_client_task(gpu_device):
         def get_client_conf(self, client_id):
             return {"learning_rate": 0.05}
 
+        def CLIENT_PING(self, request, context):  # the UPDATE_MODEL branch, aggregator.py:902-907
+            self.individual_client_events[request.executor_id].popleft()
+            return self.serialize_response(self.model_wrapper.get_weights())
+
     class Agg(DeviceAggregator, Aggregator):
         pass
 
     agg = Agg(adapter, args)
     agg.resource_manager = types.SimpleNamespace(get_next_task=lambda e: 100 + e)
+    agg.individual_client_events = {0: __import__("collections").deque(["update_model"] * 2)}
+    ping = types.SimpleNamespace(executor_id=0, client_id=0)
     conf, h0 = agg.create_client_task(3)
     assert conf == {"client_id": 103, "task_config": {"learning_rate": 0.05}}
     assert isinstance(h0, EgressHandle)
@@ -476,6 +482,7 @@ def test_egress_handles_from_create_client_task(gpu_device):
     assert b0 is h0.egress_payload and b0 is agg.serialize_response(agg.get_test_config(5)[1])
     w0 = adapter.get_weights()
     assert_state_equal(pickle.loads(b0), w0, "handle bytes r-init")
+    assert agg.CLIENT_PING(ping, None) is b0  # UPDATE_MODEL: the cached bytes, no clone
     for r, ks in sc.rounds():
         agg.start_round(len(ks))
         for res in sc.results(ks, r):
@@ -483,6 +490,7 @@ def test_egress_handles_from_create_client_task(gpu_device):
         h = agg.create_client_task(0)[1]
         assert_state_equal(list(h), adapter.get_weights(), f"handle as list r{r}")
         assert len(h) == len(w0) and torch.equal(h[0], adapter.get_weights()[0])
+    assert agg.CLIENT_PING(ping, None) is agg.serialize_response(agg.create_client_task(0)[1])
     # the first handle still serialises (and reads) as the version it was made from
     assert agg.serialize_response(h0) is b0
     assert_state_equal(list(h0), w0, "old handle")

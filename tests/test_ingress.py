@@ -260,3 +260,80 @@ def test_small_payloads_take_pickle_loads(monkeypatch):
     big = pickle.dumps(_executor_result(scale=64))
     assert len(big) >= 1 << 20
     assert not ingress.loads(big)["update_weight"]["fc.weight"].flags.writeable
+
+
+def test_client_ping_update_model_hands_out_the_egress_handle():
+    """The reference servicer's UPDATE_MODEL branch (aggregator.py:902-907) serialises
+    model_wrapper.get_weights(): under the mixin that one call returns the adapter's EgressHandle (no
+    clone); other events, other threads, the opt-out and a plugin's own CLIENT_PING keep get_weights()."""
+    import collections
+    import threading
+    import types
+
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregatorMixin
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    class FakeAdapter(TorchModelAdapter):  # only the egress part of the adapter
+        def __init__(self):
+            self.clones = 0
+
+        def egress_handle(self):
+            return "HANDLE"
+
+        def _host_copy(self):
+            self.clones += 1
+            raise LookupError("clone path")
+
+    class Aggregator:  # the shape of the reference CLIENT_PING (aggregator.py:870-912)
+        def CLIENT_PING(self, request, context):
+            ev = self.individual_client_events[request.executor_id].popleft()
+            if ev == "update_model":
+                try:
+                    data = self.model_wrapper.get_weights()
+                except LookupError:
+                    data = "CLONE"
+                # a second call in the same ping is not covered by the one-shot
+                try:
+                    self.model_wrapper.get_weights()
+                except LookupError:
+                    pass
+                return ev, data
+            return ev, None
+
+    class Agg(DeviceAggregatorMixin, Aggregator):
+        pass
+
+    agg = Agg()
+    agg.model_wrapper = FakeAdapter()
+    agg.individual_client_events = {1: collections.deque(["update_model", "model_test", "update_model"])}
+    req = types.SimpleNamespace(executor_id=1, client_id=1)
+    assert agg.CLIENT_PING(req, None) == ("update_model", "HANDLE")
+    assert agg.model_wrapper.clones == 1  # the second get_weights() cloned
+    assert agg.CLIENT_PING(req, None) == ("model_test", None)
+    out = []
+    t = threading.Thread(target=lambda: out.append(agg.CLIENT_PING(req, None)))
+    t.start()
+    t.join()
+    assert out == [("update_model", "HANDLE")]
+    # the flag does not leak out of the ping
+    try:
+        agg.model_wrapper.get_weights()
+    except LookupError:
+        pass
+    assert agg.model_wrapper.clones == 3
+    agg.device_egress_handles = False
+    agg.individual_client_events[1].append("update_model")
+    assert agg.CLIENT_PING(req, None) == ("update_model", "CLONE")
+
+    class PluginPing:
+        def CLIENT_PING(self, request, context):
+            return "plugin", None
+
+    class Wrapped(DeviceAggregatorMixin, PluginPing):
+        pass
+
+    w = Wrapped()
+    w.model_wrapper = FakeAdapter()
+    w.individual_client_events = {1: collections.deque(["update_model"])}
+    assert w.CLIENT_PING(req, None) == ("plugin", None)
+    assert w.individual_client_events[1] == collections.deque(["update_model"])
