@@ -160,9 +160,10 @@ def test_async_ingress_staging_matches_reference(gpu_device, name):
 @pytest.mark.parametrize("name", ["fedavg_femnist_cnn_k10", "fedavg_wide_k64", "fedyogi_wide_3rounds"])
 def test_zero_copy_payload_ingress_matches_reference(gpu_device, name, monkeypatch):
     """Executor payloads (pickle.dumps of the result, torch_client.py:76-91) through the mixin's
-    deserialize_response (fedscale_amd/ingress.py: arrays as read-only views of the payload) into the
-    device round: results stay those of the reference fixture, and the fast path really ran."""
+    deserialize_response (fedscale_amd/ingress.py: arrays as read-only views of the payload; every other
+    one decoded on arrival by add_event_handler on a servicer thread) into the device round: results stay those of the reference fixture, and the fast path really ran."""
     import pickle
+    import threading
 
     from fedscale_amd import ingress
     from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
@@ -177,13 +178,20 @@ def test_zero_copy_payload_ingress_matches_reference(gpu_device, name, monkeypat
     opt = TorchServerOptimizer(args.gradient_policy, args, "cuda:0") if sc.meta.get("optimizer") else None
     adapter = TorchModelAdapter(StateDictModule(sc.names, sc.init_state()), optimizer=opt, device="cuda:0")
     agg = DeviceAggregator(adapter, args)
+    agg.device_decode_on_arrival = True
     policy = sc.meta["policy"]
     for r, ks in sc.rounds():
         if policy == "q-fedavg":
             args.learning_rate = sc.meta["lrs"][r]
         agg.start_round(len(ks))
-        for res in sc.results(ks, r):
-            got_res = agg.deserialize_response(pickle.dumps(res))
+        for i, res in enumerate(sc.results(ks, r)):
+            if i % 2:  # decoded on arrival by a servicer thread (add_event_handler), popped by the main loop
+                th = threading.Thread(target=agg.add_event_handler, args=(i, "upload_model", None, pickle.dumps(res)))
+                th.start()
+                th.join()
+                got_res = agg.deserialize_response(agg.server_events_queue.popleft()[3])
+            else:
+                got_res = agg.deserialize_response(pickle.dumps(res))
             uw = got_res["update_weight"]
             views = [v for v in (uw.values() if isinstance(uw, dict) else uw)
                      if isinstance(v, np.ndarray) and v.nbytes >= 256]

@@ -337,3 +337,74 @@ def test_client_ping_update_model_hands_out_the_egress_handle():
     w.individual_client_events = {1: collections.deque(["update_model"])}
     assert w.CLIENT_PING(req, None) == ("plugin", None)
     assert w.individual_client_events[1] == collections.deque(["update_model"])
+
+
+def test_upload_decoded_on_arrival_by_the_servicer_thread():
+    """add_event_handler (aggregator.py:830-840) runs on the servicer thread: an UPLOAD_MODEL payload is
+    decoded there and the main loop's deserialize_response (:993-994) hands the result back; other events,
+    undecodable payloads, the opt-out and a plugin's own deserialize_response keep the raw bytes."""
+    import collections
+    import threading
+
+    import numpy as np
+
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregatorMixin
+
+    class Aggregator:  # the reference methods the mixin wraps
+        def __init__(self):
+            self.server_events_queue = collections.deque()
+
+        def add_event_handler(self, client_id, event, meta, data):
+            self.server_events_queue.append((client_id, event, meta, data))
+
+        def deserialize_response(self, responses):
+            return pickle.loads(responses)
+
+    class Agg(DeviceAggregatorMixin, Aggregator):
+        pass
+
+    rng = np.random.default_rng(3)
+    upd = {"w": rng.standard_normal((512, 1024), dtype=np.float32), "n": np.array(7, dtype=np.int64)}
+    res = {"client_id": 4, "update_weight": upd, "moving_loss": 0.5}
+    payload = pickle.dumps(res, protocol=4)
+    agg = Agg()
+    agg.add_event_handler(9, "upload_model", None, payload)  # off by default: the reference's queue entry
+    assert agg.server_events_queue.popleft()[3] is payload
+    agg.device_decode_on_arrival = True
+    t = threading.Thread(target=agg.add_event_handler, args=(4, "upload_model", "meta", payload))
+    t.start()
+    t.join()
+    agg.add_event_handler(4, "model_test", "meta", pickle.dumps({"acc": 1.0}))
+    agg.add_event_handler(5, "upload_model", "meta", payload[:-9])  # truncated: queued as it came
+    (c, ev, meta, data), (_, ev2, _, data2), (_, _, _, data3) = agg.server_events_queue
+    assert (c, ev, meta) == (4, "upload_model", "meta") and type(data) is not bytes
+    got = agg.deserialize_response(data)
+    assert got["client_id"] == 4 and np.array_equal(got["update_weight"]["w"], upd["w"])
+    assert got["update_weight"]["n"] == 7
+    assert type(data2) is bytes and agg.deserialize_response(data2) == {"acc": 1.0}
+    assert data3 == payload[:-9]
+    with pytest.raises(Exception):
+        agg.deserialize_response(data3)
+    agg.device_decode_on_arrival = False
+    agg.add_event_handler(6, "upload_model", None, payload)
+    assert agg.server_events_queue[-1][3] is payload
+
+    class Converting(Aggregator):  # e.g. aggregator_tflite.py:47-58
+        def deserialize_response(self, responses):
+            return ("converted", pickle.loads(responses)["client_id"])
+
+    class Wrapped(DeviceAggregatorMixin, Converting):
+        pass
+
+    w = Wrapped()
+    w.device_decode_on_arrival = True
+    w.add_event_handler(1, "upload_model", None, payload)
+    assert w.server_events_queue[0][3] is payload and w.deserialize_response(payload) == ("converted", 4)
+
+    class Standalone(DeviceAggregatorMixin):
+        pass
+
+    s = Standalone()
+    s.device_decode_on_arrival = True
+    s.add_event_handler(1, "upload_model", None, payload)
+    assert s.deserialize_response(s.server_events_queue[0][3])["client_id"] == 4

@@ -31,6 +31,10 @@ def main():
     # ... with the gather + H2D of each update on a background thread (ClientStaging(async_ingress=True)):
     # with no big copy left in deserialize_response, the main thread's next unpickle overlaps the gather
     allout.append(run(K, rounds, which, None, loader="zerocopy", async_ingress=True))
+    # the mixin's add_event_handler: a servicer thread decodes each upload on arrival and queues it, the
+    # main loop pops the queue (aggregator.py:958-959, 830-840, 984-994)
+    allout.append(run(K, rounds, which, None, loader="arrival"))
+    allout.append(run(K, rounds, which, None, loader="arrival", async_ingress=True))
     allout.append(egress(which))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     json.dump(allout, open(os.path.join(ROOT, "gpurun_out", f"ingress_{which}_k{K}.json"), "w"), indent=1)
@@ -80,7 +84,24 @@ def run(K, rounds, which, workers, loader=None, async_ingress=False):
         t0 = time.perf_counter()
         agg.start_round(K)
         t_ing = 0.0
-        for k in range(K):
+        if loader == "arrival":
+            import collections
+            import threading
+
+            agg.server_events_queue = collections.deque()
+            agg.device_decode_on_arrival = True
+            th = threading.Thread(target=lambda: [agg.add_event_handler(k, "upload_model", None, payloads[k % 8])
+                                                  for k in range(K)])
+            th.start()
+            done = 0
+            while done < K:
+                if agg.server_events_queue:
+                    agg.on_result(agg.deserialize_response(agg.server_events_queue.popleft()[3]))
+                    done += 1
+                else:
+                    time.sleep(0)
+            th.join()
+        for k in range(K if loader != "arrival" else 0):
             if payloads is not None:
                 agg.on_result(load(payloads[k % 8]))
             else:
