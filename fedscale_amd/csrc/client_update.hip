@@ -49,7 +49,10 @@ typedef float f4 __attribute__((ext_vector_type(4)));
 
 constexpr int MT_MAX = 64;               // tensors per launch (kernel-argument table 2.8 KiB, < 4 KiB; `vec` is 64 bits)
 constexpr int MT_THREADS = 256;
-constexpr int MT_UNROLL = 4;             // float4 per thread per chunk
+#ifndef MT_UNROLL_N
+#define MT_UNROLL_N 4
+#endif
+constexpr int MT_UNROLL = MT_UNROLL_N;   // float4 per thread per chunk
 constexpr int64_t MT_CHUNK = MT_THREADS * 4 * MT_UNROLL;  // 4096 elements per workgroup
 
 struct MtList {
