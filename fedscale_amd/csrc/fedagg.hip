@@ -596,6 +596,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       D[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.delta)[c0 + 64 * j]
                                                   : f4{0.f, 0.f, 0.f, 0.f};
     }
+#if QF_PIPE
     // row slice of client k (k >= K: an empty range, the loads return zeros and touch no memory)
     auto load_rows = [&](f4(&dst)[QF_V], int k) {
       if (WIDE) {
@@ -613,6 +614,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
         for (int j = 0; j < QF_V; ++j) dst[j] = rows_load(rr, voff[j]);
       }
     };
+#endif
     // one client: g = (L - W)/lr from its loaded row slice t (overwritten with L - W), delta chain and the
     // lane's fp64 sum of squares
     auto client = [&](f4(&t)[QF_V], int kk, float al) -> double {
