@@ -124,6 +124,11 @@ class OracleModel:
             dst.copy_(new[n])
 
 
+
+def _as_numpy(x):
+    """np.array(x) of the reference without numpy's __array__(copy=...) deprecation path for tensors."""
+    return x.detach().cpu().numpy() if isinstance(x, torch.Tensor) else x
+
 class OracleServerOptimizer:
     """optimizers.py:16-108 with ``device=None`` (the reference aggregator runs on CPU)."""
 
@@ -138,7 +143,7 @@ class OracleServerOptimizer:
         if self.mode == "fed-yogi":
             steps = self.gradient_controller.update([c - l for l, c in zip(last_model, current_model)])
             target_model.load_state_dict({
-                n: torch.from_numpy(np.array(last_model[i] + steps[i], dtype=np.float32))
+                n: torch.from_numpy(np.array(_as_numpy(last_model[i] + steps[i]), dtype=np.float32))
                 for i, n in enumerate(names)})
         elif self.mode == "q-fedavg":
             lr, q = self.args.learning_rate, self.args.qfed_q
