@@ -8,6 +8,9 @@ reference's fp32 arithmetic:
 
     param.data += conf.learning_rate * conf.proxy_mu * (param.data - global_model[idx])
 
+``step_and_update(optimizer, conf, model, global_model)`` fuses the executor's preceding
+``torch.optim.SGD.step()`` (torch_client.py:236) into the same pass (``fa_sgd_prox_step``).
+
 The parameters and ``global_model`` must live on the GPU (an executor training on the MI355X); there is
 no CPU fallback.  Any ``gradient_policy`` other than ``'fed-prox'`` is a no-op, as in the reference.
 """
@@ -29,3 +32,48 @@ class ClientOptimizer(object):
                 raise ValueError("fed-prox needs global_model: one tensor per model parameter")
             # the Python double lr*mu multiplies fp32 tensors, so torch rounds it to fp32 first
             kx.prox_update(params, global_model, float(conf.learning_rate * conf.proxy_mu))
+
+    def step_and_update(self, optimizer, conf, model, global_model=None, fma=True):
+        """torch_client.py:236-240, ``optimizer.step()`` then ``update_client_weight(conf, model,
+        global_model)``, as one multi-tensor launch per parameter group (``fa_sgd_prox_step``): one pass
+        over param, grad, momentum buffer and global model instead of torch's SGD passes plus the proximal
+        pass. ``optimizer`` is the ``torch.optim.SGD`` of get_optimizer (torch_client.py:95-130); its
+        momentum buffers stay in ``optimizer.state``, so it can still be stepped directly. Any other
+        optimizer (Adam for 'nlp', maximize / differentiable SGD) takes the two reference calls."""
+        import torch
+
+        prox = conf.gradient_policy == 'fed-prox'
+        params = list(model.parameters())
+        if prox and (global_model is None or len(global_model) != len(params)):
+            raise ValueError("fed-prox needs global_model: one tensor per model parameter")
+        if type(optimizer) is not torch.optim.SGD or any(
+                g.get('maximize', False) or g.get('differentiable', False) for g in optimizer.param_groups):
+            optimizer.step()
+            return self.update_client_weight(conf, model, global_model)
+        gmap = {id(p): global_model[i] for i, p in enumerate(params)} if prox else {}
+        c = float(conf.learning_rate * conf.proxy_mu) if prox else 0.0
+        stepped = set()
+        for group in optimizer.param_groups:
+            mom = float(group['momentum'])
+            ps = [p for p in group['params'] if p.grad is not None]
+            parts = {True: [], False: []}  # first step of the momentum buffer / later steps
+            for p in ps:
+                st = optimizer.state[p]
+                parts[mom != 0 and st.get('momentum_buffer') is None].append(p)
+            for first, part in parts.items():
+                if not part:
+                    continue
+                bufs = None
+                if mom != 0:
+                    if first:
+                        for p in part:
+                            optimizer.state[p]['momentum_buffer'] = torch.empty_like(p, memory_format=torch.contiguous_format)
+                    bufs = [optimizer.state[p]['momentum_buffer'] for p in part]
+                kx.sgd_prox_step(part, [p.grad for p in part], bufs, [gmap[id(p)] for p in part] if prox else None,
+                                 group['lr'], mom, group['dampening'], group['weight_decay'], group['nesterov'],
+                                 first, c, fma=fma)
+                stepped.update(id(p) for p in part)
+        if prox:  # parameters without a gradient still take the proximal step (optimizers.py:8-10)
+            rest = [(p, global_model[i]) for i, p in enumerate(params) if id(p) not in stepped]
+            if rest:
+                kx.prox_update([p for p, _ in rest], [g for _, g in rest], c)

@@ -139,6 +139,87 @@ __global__ __launch_bounds__(MT_THREADS) void k_prox(MtList L, float c) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Local SGD step fused with the FedProx step (torch_client.py:236-240): torch.optim.SGD(lr, momentum,
+// dampening, weight_decay, nesterov) on every parameter, then p += c * (p - g) (optimizers.py:10).
+// One pass over param, grad, momentum buffer and global model instead of torch's foreach SGD passes
+// plus the proximal pass.  `fma`: torch's alpha-adds (add(x, alpha=a), mul_().add_()) as one fused
+// multiply-add each, the way its elementwise kernels are contracted on ROCm; 0: every op rounded.
+// ------------------------------------------------------------------------------------------------
+struct SgdList {
+  float* p[MT_MAX];
+  const float* g[MT_MAX];      // gradient
+  float* m[MT_MAX];            // momentum buffer (NULL when momentum == 0)
+  const float* w[MT_MAX];      // global model (NULL: no proximal step)
+  int64_t n[MT_MAX];
+  int32_t blk0[MT_MAX + 1];
+  uint64_t vec;
+  int32_t T;
+};
+struct SgdScalars {
+  float lr, momentum, dampening, wd, c;
+  int32_t nesterov, first, fma, prox;
+};
+__device__ __forceinline__ float axpy(float a, float x, float y, int fma) {  // y + a * x
+  return fma ? __builtin_fmaf(a, x, y) : y + a * x;
+}
+__device__ __forceinline__ void sgd1(float& p, float g, float& m, float w, const SgdScalars& k) {
+  float d = g;
+  if (k.wd != 0.f) d = axpy(k.wd, p, d, k.fma);                 // grad.add(param, alpha=weight_decay)
+  if (k.momentum != 0.f) {
+    m = k.first ? d : axpy(1.f - k.dampening, d, m * k.momentum, k.fma);  // buf.mul_(mom).add_(d, alpha=1-damp)
+    d = k.nesterov ? axpy(k.momentum, m, d, k.fma) : m;         // d.add(buf, alpha=mom) / buf
+  }
+  p = axpy(-k.lr, d, p, k.fma);                                 // param.add_(d, alpha=-lr)
+  if (k.prox) p = p + k.c * (p - w);                            // optimizers.py:10 (separate torch ops)
+}
+__global__ __launch_bounds__(MT_THREADS) void k_sgd_prox(SgdList L, SgdScalars k) {
+  int lo = 0, hi = L.T - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (L.blk0[mid] <= (int)blockIdx.x) lo = mid; else hi = mid - 1;
+  }
+  const int t = lo;
+  const int64_t n = L.n[t];
+  const int64_t e0 = (int64_t)(blockIdx.x - L.blk0[t]) * MT_CHUNK;
+  float* __restrict__ p = L.p[t];
+  const float* __restrict__ g = L.g[t];
+  float* __restrict__ m = L.m[t];
+  const float* __restrict__ w = L.w[t];
+  const bool hasm = k.momentum != 0.f;
+  if ((L.vec >> t) & 1) {
+#pragma unroll
+    for (int u = 0; u < MT_UNROLL; ++u) {
+      const int64_t i = e0 + ((int64_t)u * MT_THREADS + threadIdx.x) * 4;
+      if (i + 4 <= n) {
+        f4 P = *(const f4*)(p + i), G = *(const f4*)(g + i);
+        f4 M = (hasm && !k.first) ? *(const f4*)(m + i) : f4{0.f, 0.f, 0.f, 0.f};
+        const f4 W = k.prox ? *(const f4*)(w + i) : f4{0.f, 0.f, 0.f, 0.f};
+        float pv[4] = {P.x, P.y, P.z, P.w}, mv[4] = {M.x, M.y, M.z, M.w};
+        const float gv[4] = {G.x, G.y, G.z, G.w}, wv[4] = {W.x, W.y, W.z, W.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sgd1(pv[e], gv[e], mv[e], wv[e], k);
+        P = f4{pv[0], pv[1], pv[2], pv[3]};
+        M = f4{mv[0], mv[1], mv[2], mv[3]};
+        *(f4*)(p + i) = P;
+        if (hasm) *(f4*)(m + i) = M;
+      } else {
+        for (int64_t j = i; j < n && j < i + 4; ++j) {
+          float mj = (hasm && !k.first) ? m[j] : 0.f;
+          sgd1(p[j], g[j], mj, k.prox ? w[j] : 0.f, k);
+          if (hasm) m[j] = mj;
+        }
+      }
+    }
+  } else {
+    for (int64_t j = e0 + threadIdx.x; j < n && j < e0 + MT_CHUNK; j += MT_THREADS) {
+      float mj = (hasm && !k.first) ? m[j] : 0.f;
+      sgd1(p[j], g[j], mj, k.prox ? w[j] : 0.f, k);
+      if (hasm) m[j] = mj;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // DP, pass 1: per-workgroup partial of sum((a - b)^2) (norm_type 2) or max|a - b| (inf) in fp64
 // ------------------------------------------------------------------------------------------------
 // max that propagates NaN, like torch.max (fmax would drop it)
@@ -375,6 +456,52 @@ extern "C" int fa_prox_update(float* const* param, const float* const* global, c
     if (grid == 0) continue;
     hipLaunchKernelGGL(k_prox, dim3(grid), dim3(MT_THREADS), 0, (hipStream_t)stream, L, c);
     if ((rc = check_launch("fa_prox_update"))) return rc;
+  }
+  return FA_OK;
+}
+
+extern "C" int fa_sgd_prox_step(float* const* param, const float* const* grad, float* const* momentum_buf,
+                                const float* const* global, const int64_t* numel, int32_t T, float lr,
+                                float momentum, float dampening, float weight_decay, int32_t nesterov,
+                                int32_t first, float c, int32_t fma, fa_stream_t stream) {
+  int rc = check_list("fa_sgd_prox_step", T, param, grad, numel, true);
+  if (rc) return rc;
+  for (int i = 0; i < T; ++i) {
+    if (numel[i] == 0) continue;
+    if (momentum != 0.f && (!momentum_buf || !momentum_buf[i]))
+      return fail(FA_E_ARG, "fa_sgd_prox_step: tensor %d: momentum != 0 needs a momentum buffer", i);
+    if (global && !global[i]) return fail(FA_E_ARG, "fa_sgd_prox_step: tensor %d: NULL global pointer", i);
+    if ((momentum_buf && ((uintptr_t)momentum_buf[i] & 3u)) || (global && ((uintptr_t)global[i] & 3u)))
+      return fail(FA_E_ARG, "fa_sgd_prox_step: tensor %d: pointers must be 4-byte aligned", i);
+  }
+  if (nesterov && (momentum <= 0.f || dampening != 0.f))
+    return fail(FA_E_ARG, "fa_sgd_prox_step: nesterov needs momentum > 0 and zero dampening");
+  SgdScalars k{lr, momentum, dampening, weight_decay, c, nesterov ? 1 : 0, first ? 1 : 0, fma ? 1 : 0,
+               global ? 1 : 0};
+  int32_t t = 0;
+  while (t < T) {
+    SgdList L;
+    L.T = 0;
+    L.vec = 0;
+    int32_t blk = 0;
+    while (t < T && L.T < MT_MAX) {
+      const int64_t nb = (numel[t] + MT_CHUNK - 1) / MT_CHUNK;
+      if (L.T > 0 && blk + nb > (int64_t)INT32_MAX / 2) break;
+      L.p[L.T] = param[t];
+      L.g[L.T] = grad[t];
+      L.m[L.T] = (momentum != 0.f) ? momentum_buf[t] : nullptr;
+      L.w[L.T] = global ? global[t] : nullptr;
+      L.n[L.T] = numel[t];
+      L.blk0[L.T] = blk;
+      if (al16(L.p[L.T]) && al16(L.g[L.T]) && al16(L.m[L.T]) && al16(L.w[L.T])) L.vec |= (uint64_t)1 << L.T;
+      blk += (int32_t)nb;
+      ++L.T;
+      ++t;
+    }
+    L.blk0[L.T] = blk;
+    if (blk == 0) continue;
+    hipLaunchKernelGGL(k_sgd_prox, dim3(blk), dim3(MT_THREADS), 0, (hipStream_t)stream, L, k);
+    if ((rc = check_launch("fa_sgd_prox_step"))) return rc;
   }
   return FA_OK;
 }

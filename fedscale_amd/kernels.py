@@ -262,6 +262,40 @@ def prox_update(params, global_model, c: float):
          _stream(params[0]))
 
 
+def sgd_prox_step(params, grads, bufs, global_model, lr: float, momentum: float, dampening: float,
+                  weight_decay: float, nesterov: bool, first: bool, c: float, fma: bool = True):
+    """torch.optim.SGD step + FedProx step over every tensor in one multi-tensor launch (fa_sgd_prox_step).
+    ``bufs`` None when momentum == 0; ``global_model`` None: no proximal step."""
+    params, grads = list(params), list(grads)
+    if not params:
+        return
+    bufs = list(bufs) if bufs is not None else None
+    global_model = list(global_model) if global_model is not None else None
+    if momentum != 0 and bufs is None:
+        raise ValueError("momentum != 0 needs momentum buffers")
+
+    def build():
+        dev = _fp32_list(params, "param")
+        for name, lst in (("grad", grads), ("momentum_buffer", bufs), ("global_model", global_model)):
+            if lst is None:
+                continue
+            if len(lst) != len(params):
+                raise ValueError(f"{len(params)} parameters but {len(lst)} {name} tensors")
+            _fp32_list(lst, name, dev)
+            for i, (p, t) in enumerate(zip(params, lst)):
+                if p.shape != t.shape:
+                    raise ValueError(f"{name}[{i}] shape {tuple(t.shape)} != param[{i}] shape {tuple(p.shape)}")
+        return _Plan([params, grads, bufs if bufs is not None else [None] * len(params),
+                      global_model if global_model is not None else [None] * len(params)],
+                     [p.numel() for p in params])
+
+    plan = _cached_plan("sgdprox", (params, grads, bufs, global_model), build)
+    call("fa_sgd_prox_step", plan.ptr(0), plan.ptr(1), plan.ptr(2) if bufs is not None else None,
+         plan.ptr(3) if global_model is not None else None, plan.numel.ctypes.data, plan.T, float(lr),
+         float(momentum), float(dampening), float(weight_decay), int(bool(nesterov)), int(bool(first)), float(c),
+         int(bool(fma)), _stream(params[0]))
+
+
 def dp_clip_coef(params, last, max_norm: float, norm_inf: bool, coef_out: torch.Tensor):
     """coef_out[0:3] <- (total norm of param - last, clip coefficient, apply flag) (fa_dp_clip_coef)."""
     params = list(params)

@@ -39,6 +39,20 @@ int fa_prox_update(float* const* param, const float* const* global, const int64_
                    fa_stream_t stream);
 
 /*
+ * One local training step fused with the FedProx step: replaces torch_client.py:236-240
+ * (torch.optim.SGD.step() as built by get_optimizer :95-130, then update_client_weight, optimizers.py:6-10).
+ * Per element of every tensor t, as torch.optim.SGD (maximize False) then FedProx:
+ *   d = grad + weight_decay * p;  buf = first ? d : buf * momentum + (1 - dampening) * d;
+ *   d = nesterov ? d + momentum * buf : buf;  p = p - lr * d;  p = p + c * (p - global)
+ * momentum_buf[t] is written (read unless `first`); ignored when momentum == 0.  global == NULL: no
+ * proximal step.  fma != 0: each alpha-add is one fused multiply-add (torch's elementwise kernels on ROCm).
+ */
+int fa_sgd_prox_step(float* const* param, const float* const* grad, float* const* momentum_buf,
+                     const float* const* global, const int64_t* numel, int32_t T, float lr, float momentum,
+                     float dampening, float weight_decay, int32_t nesterov, int32_t first, float c, int32_t fma,
+                     fa_stream_t stream);
+
+/*
  * Local-DP clipping coefficient, examples/differential_privacy/clip_norm.py:12-52 applied to
  * delta[t] = param[t] - last[t] (customized_client.py:51-55; last[t] == NULL: delta[t] = param[t]):
  *   norms[t] = ||delta[t]||_2 (fp32)  ->  total = ||stack(norms)||_2   (norm_inf: max |delta|)

@@ -260,3 +260,60 @@ def test_client_optimizer_on_a_real_module(gpu_device):
     snap = [p.data.clone() for p in net.parameters()]
     opt.update_client_weight(conf, net, glob)
     assert all(torch.equal(a, b.data) for a, b in zip(snap, net.parameters()))
+
+
+def _sgd_model(seed, device):
+    g = torch.Generator().manual_seed(seed)
+    shapes = [(64, 3, 3, 3), (64,), (10, 4097), (10,), (5, 7), (3,)]  # ragged, non-multiple-of-4 tails
+    m = torch.nn.Module()
+    for i, s in enumerate(shapes):
+        m.register_parameter(f"p{i}", torch.nn.Parameter(torch.randn(s, generator=g).to(device)))
+    return m, g
+
+
+@pytest.mark.parametrize("momentum,nesterov,wd,damp", [(0.9, False, 5e-4, 0.0), (0.0, False, 5e-4, 0.0),
+                                                       (0.9, True, 1e-3, 0.0), (0.5, False, 0.0, 0.1)])
+def test_fused_sgd_prox_step_matches_torch_sgd_then_fedprox(gpu_device, momentum, nesterov, wd, damp):
+    """ClientOptimizer.step_and_update == torch.optim.SGD.step() + update_client_weight (torch_client.py:
+    236-240, optimizers.py:6-10) over 4 local steps, one parameter without a gradient: parameters and
+    momentum buffers within the north-star fp32 tolerance (rtol 1e-5, atol 1e-6) for both variants, and
+    bit-exact to torch's foreach SGD on the GPU with fma (the default: torch's alpha-adds are contracted)."""
+    import argparse
+    import copy
+
+    from fedscale_amd.cloud.execution.optimizers import ClientOptimizer
+
+    conf = argparse.Namespace(gradient_policy="fed-prox", learning_rate=0.05, proxy_mu=0.1)
+    ref, g = _sgd_model(7, gpu_device)
+    glob = [p.detach().clone() + 0.01 for p in ref.parameters()]
+    exact = {}
+    for fma in (True, False):
+        ours = copy.deepcopy(ref)
+        r = copy.deepcopy(ref)
+        kw = dict(lr=conf.learning_rate, momentum=momentum, weight_decay=wd, nesterov=nesterov, dampening=damp)
+        opt_r, opt_o = torch.optim.SGD(r.parameters(), **kw), torch.optim.SGD(ours.parameters(), **kw)
+        gg = torch.Generator().manual_seed(11)
+        for step in range(4):
+            for i, (pr, po) in enumerate(zip(r.parameters(), ours.parameters())):
+                if i == 3:  # no gradient: SGD skips it, FedProx still moves it
+                    pr.grad = po.grad = None
+                    continue
+                gr = torch.randn(pr.shape, generator=gg).to(gpu_device)
+                pr.grad, po.grad = gr.clone(), gr.clone()
+            opt_r.step()
+            for idx, param in enumerate(r.parameters()):  # optimizers.py:8-10, literally
+                param.data += conf.learning_rate * conf.proxy_mu * (param.data - glob[idx])
+            ClientOptimizer().step_and_update(opt_o, conf, ours, glob, fma=fma)
+        torch.cuda.synchronize()
+        ok = True
+        for pr, po in zip(r.parameters(), ours.parameters()):
+            torch.testing.assert_close(po.detach(), pr.detach(), rtol=1e-5, atol=1e-6)
+            ok &= torch.equal(po.detach(), pr.detach())
+            if momentum != 0 and pr.grad is not None:
+                br, bo = opt_r.state[pr]["momentum_buffer"], opt_o.state[po]["momentum_buffer"]
+                torch.testing.assert_close(bo, br, rtol=1e-5, atol=1e-6)
+                ok &= torch.equal(bo, br)
+        exact[fma] = ok
+    assert exact[True], "fma variant: expected bit-exact to torch SGD + FedProx on the GPU"
+    print(f"[sgd-prox] momentum={momentum} nesterov={nesterov} wd={wd} damp={damp}: bit-exact vs torch on GPU "
+          f"fma={exact[True]} rounded={exact[False]}")
