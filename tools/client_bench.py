@@ -118,6 +118,32 @@ def main():
                 "torch_per_tensor_gpu_ms": ms_ref, "speedup_vs_torch_gpu": ms_ref / ms,
                 "reference_cpu_ms": ms_cpu, "cpu_threads": torch.get_num_threads()})
 
+    # ---- local SGD step + FedProx (torch_client.py:236-240) ------------------------------------
+    import argparse
+
+    from fedscale_amd.cloud.execution.optimizers import ClientOptimizer
+
+    conf = argparse.Namespace(gradient_policy="fed-prox", learning_rate=lr, proxy_mu=mu)
+    for p in net.parameters():
+        p.grad = torch.randn_like(p) * 0.01
+    sgd_kw = dict(lr=lr, momentum=0.9, weight_decay=5e-4)  # get_optimizer's default (:127-128)
+    opt_ref = torch.optim.SGD(net.parameters(), **sgd_kw)
+
+    def ref_step():
+        opt_ref.step()
+        ref_prox(params, glob, lr, mu)
+
+    ms_sgd_ref = timed_events(ref_step, reps, stream)
+    opt_dev = torch.optim.SGD(net.parameters(), **sgd_kw)
+    co = ClientOptimizer()
+    ms_sgd = timed_events(lambda: co.step_and_update(opt_dev, conf, net, glob), reps, stream)
+    wall_sgd = timed_wall(lambda: co.step_and_update(opt_dev, conf, net, glob), reps)
+    alg = 24 * P  # read param, grad, momentum buffer, global model; write param, momentum buffer
+    out.append({"handler": "sgd_fedprox_step", "layout": "resnet18_cifar10", "params": P,
+                "device_ms": ms_sgd, "device_wall_ms_incl_host": wall_sgd, "alg_bytes": alg,
+                "device_gbps": alg / (ms_sgd * 1e-3) / 1e9,
+                "torch_sgd_plus_prox_gpu_ms": ms_sgd_ref, "speedup_vs_torch_gpu": ms_sgd_ref / ms_sgd})
+
     # ---- local DP ----------------------------------------------------------------------------
     last = [p.clone() for p in params]
     with torch.no_grad():
