@@ -41,6 +41,25 @@ def test_error_path_without_gpu():
         call("fa_reduce", None, 6, 1, 8, None, None, None, 1.0, 2, None)  # validation precedes any HIP call
 
 
+def test_sgd_prox_step_argument_errors_without_gpu():
+    """fa_sgd_prox_step validates before any HIP call: momentum without buffers, nesterov with dampening,
+    misaligned pointers (fake device addresses are never dereferenced)."""
+    import ctypes
+
+    from fedscale_amd._native import FedAggError, call
+
+    arr = lambda *v: (ctypes.c_uint64 * len(v))(*v)
+    n = (ctypes.c_int64 * 1)(8)
+    with pytest.raises(FedAggError, match="momentum buffer"):
+        call("fa_sgd_prox_step", arr(256), arr(512), None, None, n, 1, 0.1, 0.9, 0.0, 0.0, 0, 1, 0.0, 1, None)
+    with pytest.raises(FedAggError, match="nesterov"):
+        call("fa_sgd_prox_step", arr(256), arr(512), arr(768), None, n, 1, 0.1, 0.9, 0.1, 0.0, 1, 1, 0.0, 1, None)
+    with pytest.raises(FedAggError, match="aligned"):
+        call("fa_sgd_prox_step", arr(256), arr(512), arr(770), None, n, 1, 0.1, 0.9, 0.0, 0.0, 0, 1, 0.0, 1, None)
+    with pytest.raises(FedAggError, match="NULL reference"):
+        call("fa_sgd_prox_step", arr(256), arr(0), None, None, n, 1, 0.1, 0.0, 0.0, 0.0, 0, 1, 0.0, 1, None)
+
+
 def test_kernels_reject_host_tensors():
     from fedscale_amd import kernels as kx
 
