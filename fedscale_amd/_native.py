@@ -58,7 +58,7 @@ SIGNATURES = {
                                      _c_void_p, _c_void_p]),
     # include/fedclient.h (client-side handlers; pointer tables are host arrays)
     "fa_prox_update": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _f32, _c_void_p]),
-    "fa_sgd_prox_step": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _f32, _f32, _f32,
+    "fa_sgd_prox_step": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _f32, _f32, _f64,
                                 _f32, _i32, _i32, _f32, _i32, _c_void_p]),
     "fa_dp_workspace_bytes": (_i64, [_c_void_p, _i32]),
     "fa_dp_clip_coef": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _f32, _i32, _c_void_p, _c_void_p,

@@ -33,6 +33,40 @@ class ClientOptimizer(object):
             # the Python double lr*mu multiplies fp32 tensors, so torch rounds it to fp32 first
             kx.prox_update(params, global_model, float(conf.learning_rate * conf.proxy_mu))
 
+    @staticmethod
+    def _fused_ok(optimizer, gmap, prox) -> bool:
+        """The fused launch covers plain torch.optim.SGD over dense, contiguous fp32 device tensors whose
+        parameters are all the model's (and have a global counterpart under fed-prox). Anything else
+        (AMP half params, channels_last, sparse grads, params outside model.parameters()) takes the two
+        reference calls, which torch and update_client_weight handle as the reference does."""
+        import torch
+
+        if type(optimizer) is not torch.optim.SGD:
+            return False
+        dev = None
+        for g in optimizer.param_groups:
+            if g.get('maximize', False) or g.get('differentiable', False):
+                return False
+            for p in g['params']:
+                if prox and id(p) not in gmap:
+                    return False
+                for t in (p, p.grad):
+                    if t is None:
+                        continue
+                    if (t.layout != torch.strided or t.dtype != torch.float32 or t.device.type != 'cuda'
+                            or not t.is_contiguous()):
+                        return False
+                    if dev is None:
+                        dev = t.device
+                    elif t.device != dev:
+                        return False
+                if prox:
+                    w = gmap[id(p)]
+                    if (not isinstance(w, torch.Tensor) or w.dtype != torch.float32 or w.device != p.device
+                            or not w.is_contiguous() or w.shape != p.shape):
+                        return False
+        return True
+
     def step_and_update(self, optimizer, conf, model, global_model=None, fma=True):
         """torch_client.py:236-240, ``optimizer.step()`` then ``update_client_weight(conf, model,
         global_model)``, as one multi-tensor launch per parameter group (``fa_sgd_prox_step``): one pass
@@ -46,11 +80,10 @@ class ClientOptimizer(object):
         params = list(model.parameters())
         if prox and (global_model is None or len(global_model) != len(params)):
             raise ValueError("fed-prox needs global_model: one tensor per model parameter")
-        if type(optimizer) is not torch.optim.SGD or any(
-                g.get('maximize', False) or g.get('differentiable', False) for g in optimizer.param_groups):
+        gmap = {id(p): global_model[i] for i, p in enumerate(params)} if prox else {}
+        if not self._fused_ok(optimizer, gmap, prox):
             optimizer.step()
             return self.update_client_weight(conf, model, global_model)
-        gmap = {id(p): global_model[i] for i, p in enumerate(params)} if prox else {}
         c = float(conf.learning_rate * conf.proxy_mu) if prox else 0.0
         stepped = set()
         for group in optimizer.param_groups:
@@ -65,13 +98,16 @@ class ClientOptimizer(object):
                     continue
                 bufs = None
                 if mom != 0:
-                    if first:
-                        for p in part:
-                            optimizer.state[p]['momentum_buffer'] = torch.empty_like(p, memory_format=torch.contiguous_format)
-                    bufs = [optimizer.state[p]['momentum_buffer'] for p in part]
+                    # new buffers enter optimizer.state only once the launch has been accepted: a call
+                    # that raises must not leave uninitialised momentum behind for the next step
+                    bufs = ([torch.empty_like(p, memory_format=torch.contiguous_format) for p in part] if first
+                            else [optimizer.state[p]['momentum_buffer'] for p in part])
                 kx.sgd_prox_step(part, [p.grad for p in part], bufs, [gmap[id(p)] for p in part] if prox else None,
                                  group['lr'], mom, group['dampening'], group['weight_decay'], group['nesterov'],
                                  first, c, fma=fma)
+                if mom != 0 and first:
+                    for p, b in zip(part, bufs):
+                        optimizer.state[p]['momentum_buffer'] = b
                 stepped.update(id(p) for p in part)
         if prox:  # parameters without a gradient still take the proximal step (optimizers.py:8-10)
             rest = [(p, global_model[i]) for i, p in enumerate(params) if id(p) not in stepped]

@@ -156,7 +156,7 @@ struct SgdList {
   int32_t T;
 };
 struct SgdScalars {
-  float lr, momentum, dampening, wd, c;
+  float lr, momentum, omd, wd, c;  // omd = fp32(1 - dampening), computed in double as torch does
   int32_t nesterov, first, fma, prox;
 };
 __device__ __forceinline__ float axpy(float a, float x, float y, int fma) {  // y + a * x
@@ -166,7 +166,7 @@ __device__ __forceinline__ void sgd1(float& p, float g, float& m, float w, const
   float d = g;
   if (k.wd != 0.f) d = axpy(k.wd, p, d, k.fma);                 // grad.add(param, alpha=weight_decay)
   if (k.momentum != 0.f) {
-    m = k.first ? d : axpy(1.f - k.dampening, d, m * k.momentum, k.fma);  // buf.mul_(mom).add_(d, alpha=1-damp)
+    m = k.first ? d : axpy(k.omd, d, m * k.momentum, k.fma);  // buf.mul_(mom).add_(d, alpha=1-damp)
     d = k.nesterov ? axpy(k.momentum, m, d, k.fma) : m;         // d.add(buf, alpha=mom) / buf
   }
   p = axpy(-k.lr, d, p, k.fma);                                 // param.add_(d, alpha=-lr)
@@ -462,7 +462,7 @@ extern "C" int fa_prox_update(float* const* param, const float* const* global, c
 
 extern "C" int fa_sgd_prox_step(float* const* param, const float* const* grad, float* const* momentum_buf,
                                 const float* const* global, const int64_t* numel, int32_t T, float lr,
-                                float momentum, float dampening, float weight_decay, int32_t nesterov,
+                                float momentum, double dampening, float weight_decay, int32_t nesterov,
                                 int32_t first, float c, int32_t fma, fa_stream_t stream) {
   int rc = check_list("fa_sgd_prox_step", T, param, grad, numel, true);
   if (rc) return rc;
@@ -474,9 +474,10 @@ extern "C" int fa_sgd_prox_step(float* const* param, const float* const* grad, f
     if ((momentum_buf && ((uintptr_t)momentum_buf[i] & 3u)) || (global && ((uintptr_t)global[i] & 3u)))
       return fail(FA_E_ARG, "fa_sgd_prox_step: tensor %d: pointers must be 4-byte aligned", i);
   }
-  if (nesterov && (momentum <= 0.f || dampening != 0.f))
+  if (nesterov && (momentum <= 0.f || dampening != 0.0))
     return fail(FA_E_ARG, "fa_sgd_prox_step: nesterov needs momentum > 0 and zero dampening");
-  SgdScalars k{lr, momentum, dampening, weight_decay, c, nesterov ? 1 : 0, first ? 1 : 0, fma ? 1 : 0,
+  // torch's buf.add_(d, alpha=1 - dampening): the Python double 1 - dampening, rounded to fp32 once
+  SgdScalars k{lr, momentum, (float)(1.0 - dampening), weight_decay, c, nesterov ? 1 : 0, first ? 1 : 0, fma ? 1 : 0,
                global ? 1 : 0};
   int32_t t = 0;
   while (t < T) {

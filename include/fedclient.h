@@ -46,10 +46,12 @@ int fa_prox_update(float* const* param, const float* const* global, const int64_
  *   d = nesterov ? d + momentum * buf : buf;  p = p - lr * d;  p = p + c * (p - global)
  * momentum_buf[t] is written (read unless `first`); ignored when momentum == 0.  global == NULL: no
  * proximal step.  fma != 0: each alpha-add is one fused multiply-add (torch's elementwise kernels on ROCm).
+ * dampening is the Python double of the param group: 1 - dampening is formed in double and rounded to
+ * fp32 once, as torch does for the alpha of buf.add_(d, alpha=1 - dampening).
  */
 int fa_sgd_prox_step(float* const* param, const float* const* grad, float* const* momentum_buf,
                      const float* const* global, const int64_t* numel, int32_t T, float lr, float momentum,
-                     float dampening, float weight_decay, int32_t nesterov, int32_t first, float c, int32_t fma,
+                     double dampening, float weight_decay, int32_t nesterov, int32_t first, float c, int32_t fma,
                      fa_stream_t stream);
 
 /*

@@ -317,3 +317,91 @@ def test_fused_sgd_prox_step_matches_torch_sgd_then_fedprox(gpu_device, momentum
     assert exact[True], "fma variant: expected bit-exact to torch SGD + FedProx on the GPU"
     print(f"[sgd-prox] momentum={momentum} nesterov={nesterov} wd={wd} damp={damp}: bit-exact vs torch on GPU "
           f"fma={exact[True]} rounded={exact[False]}")
+
+
+def test_fused_sgd_prox_step_groups_and_late_gradients(gpu_device):
+    """Several param groups with their own lr / weight_decay / momentum / dampening (the detection task
+    builds one group per parameter, torch_client.py:100-108), and a parameter whose first gradient comes at
+    step 2 (one group then holds first-step and later-step momentum buffers: two launches). Bit-exact to
+    torch.optim.SGD.step() + the reference's FedProx lines on the GPU."""
+    import argparse
+    import copy
+
+    from fedscale_amd.cloud.execution.optimizers import ClientOptimizer
+
+    conf = argparse.Namespace(gradient_policy="fed-prox", learning_rate=0.05, proxy_mu=0.1)
+    ref, _ = _sgd_model(9, gpu_device)
+    glob = [p.detach().clone() - 0.02 for p in ref.parameters()]
+    ours = copy.deepcopy(ref)
+
+    def groups(m):
+        ps = list(m.parameters())
+        return [dict(params=[ps[0], ps[3]], lr=0.05, momentum=0.9, weight_decay=5e-4, dampening=0.3),
+                dict(params=[ps[1]], lr=0.01, momentum=0.0, weight_decay=1e-3),
+                dict(params=[ps[2], ps[4]], lr=0.2, momentum=0.7, weight_decay=0.0, dampening=0.05),
+                dict(params=[ps[5]], lr=0.03, momentum=0.9, nesterov=True, weight_decay=1e-4)]
+
+    opt_r, opt_o = torch.optim.SGD(groups(ref), lr=0.1), torch.optim.SGD(groups(ours), lr=0.1)
+    gg = torch.Generator().manual_seed(3)
+    for step in range(5):
+        for i, (pr, po) in enumerate(zip(ref.parameters(), ours.parameters())):
+            if i == 3 and step < 2:  # no gradient yet: SGD skips it, FedProx still moves it
+                pr.grad = po.grad = None
+                continue
+            gr = torch.randn(pr.shape, generator=gg).to(gpu_device)
+            pr.grad, po.grad = gr.clone(), gr.clone()
+        opt_r.step()
+        for idx, param in enumerate(ref.parameters()):  # optimizers.py:8-10, literally
+            param.data += conf.learning_rate * conf.proxy_mu * (param.data - glob[idx])
+        ClientOptimizer().step_and_update(opt_o, conf, ours, glob)
+        torch.cuda.synchronize()
+        for pr, po in zip(ref.parameters(), ours.parameters()):
+            assert torch.equal(po.detach(), pr.detach()), f"step {step}: parameter differs"
+            br, bo = opt_r.state[pr].get("momentum_buffer"), opt_o.state[po].get("momentum_buffer")
+            assert (br is None) == (bo is None)
+            if br is not None:
+                assert torch.equal(bo, br), f"step {step}: momentum buffer differs"
+
+
+def test_failed_fused_step_leaves_optimizer_state_unchanged(gpu_device):
+    """A launch the library rejects (nesterov with dampening, set on the group after construction) raises
+    and leaves no uninitialised momentum buffer in optimizer.state (a later step would read it)."""
+    import argparse
+
+    from fedscale_amd._native import FedAggError
+    from fedscale_amd.cloud.execution.optimizers import ClientOptimizer
+
+    conf = argparse.Namespace(gradient_policy="fed-prox", learning_rate=0.05, proxy_mu=0.1)
+    m, _ = _sgd_model(4, gpu_device)
+    glob = [p.detach().clone() for p in m.parameters()]
+    opt = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9, nesterov=True)
+    opt.param_groups[0]["dampening"] = 0.5
+    for p in m.parameters():
+        p.grad = torch.ones_like(p)
+    with pytest.raises(FedAggError, match="nesterov"):
+        ClientOptimizer().step_and_update(opt, conf, m, glob)
+    assert all("momentum_buffer" not in opt.state[p] for p in m.parameters())
+
+
+def test_fused_step_falls_back_for_tensors_it_does_not_cover(gpu_device):
+    """channels_last parameters and params outside model.parameters() take optimizer.step() +
+    update_client_weight (the reference's two calls), with the same result as torch."""
+    import argparse
+    import copy
+
+    from fedscale_amd.cloud.execution.optimizers import ClientOptimizer
+
+    conf = argparse.Namespace(gradient_policy="fed-avg", learning_rate=0.05, proxy_mu=0.1)
+    ref = torch.nn.Conv2d(8, 8, 3).to(gpu_device).to(memory_format=torch.channels_last)
+    ours = copy.deepcopy(ref)
+    assert not ref.weight.is_contiguous()
+    opt_r = torch.optim.SGD(ref.parameters(), lr=0.1, momentum=0.9)
+    opt_o = torch.optim.SGD(ours.parameters(), lr=0.1, momentum=0.9)
+    for _ in range(2):
+        for pr, po in zip(ref.parameters(), ours.parameters()):
+            g = torch.randn_like(pr)
+            pr.grad, po.grad = g.clone(), g.clone()
+        opt_r.step()
+        ClientOptimizer().step_and_update(opt_o, conf, ours, None)
+    for pr, po in zip(ref.parameters(), ours.parameters()):
+        assert torch.equal(pr, po)

@@ -139,3 +139,60 @@ def test_c5_qfedavg_shard_k10000_streamed(gpu_device):
         assert abs(sqh[k] - ref) <= 1e-9 * ref  # fp32 partials of 4 squares, then fp64
     assert np.all(sqh > 0)
     del x
+    # the round's finish over the whole 10,000-client chain (optimizers.py:96-104): hs from the device's
+    # norms with the reference's fp32 recurrence, then new = L - delta / (hs + 1e-10), both bit-exact
+    c1 = np.array([np.float32(q * np.float_power(l + 1e-10, q - 1)) for l in losses], dtype=np.float32)
+    c2 = np.array([np.float32((1.0 / lr) * np.float_power(l + 1e-10, q)) for l in losses], dtype=np.float32)
+    hs_dev = torch.zeros(2, device="cuda")
+    new = torch.empty(ld, device="cuda")
+    kx.qfed_hs(sq, torch.from_numpy(c1).cuda(), torch.from_numpy(c2).cuda(), K, hs_dev)
+    kx.qfed_finalize(last, delta, hs_dev, new, P)
+    hs = np.float32(0.0)
+    for k in range(K):
+        hs = np.float32(hs + np.float32(c1[k] * np.float32(sqh[k]) + c2[k]))
+    hs_got = hs_dev.cpu().numpy()
+    assert hs_got[0] == hs and hs_got[1] == np.float32(hs + np.float32(1e-10))
+    want = L - d / np.float32(hs_got[1])
+    np.testing.assert_array_equal(new[torch.from_numpy(cols).cuda()].cpu().numpy(), want)
+
+
+def test_c2_synthetic_k100_p1m_fedavg_every_column(gpu_device):
+    """Config 2 at its exact shape: 100 clients x 1,000,000 fp32, FedAvg, bit-exact on ALL columns against
+    the oracle's flat restatement of aggregator.py:497-507 (sequential fp32 sum, true division by K)."""
+    from fedscale_amd import kernels as kx
+    from fedscale_amd import synth
+    from fedscale_amd.bucket import round_up
+    from oracle.cpu_reference import fedavg_flat
+
+    K, P, seed = 100, 1_000_000, 22
+    ld = round_up(P, 64)
+    x = torch.empty(K, ld, device="cuda")
+    synth.fill(x, K, P, seed=seed)
+    out = torch.empty(ld, device="cuda")
+    kx.reduce(x, K, P, out, denom=float(np.float32(K)), finalize=True)
+    want = fedavg_flat(x[:, :P].cpu().numpy())
+    np.testing.assert_array_equal(out[:P].cpu().numpy(), want)
+
+
+def test_c2_through_the_drop_in_from_host_updates(gpu_device):
+    """Config 2 through the aggregator hook: 100 host uploads of a 1M-parameter model (two tensors, one
+    ragged) staged to HBM in chunks of 30 and reduced; the global model is the oracle's mean bit for bit."""
+    from fedscale_amd import synth
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+    from oracle.cpu_reference import fedavg_close, fedavg_step
+
+    K = 100
+    names, shapes = ["w", "b"], [(999, 1001), (1_000_000 - 999 * 1001,)]
+    model = synth.LayoutModule(names, shapes, [torch.float32, torch.float32])
+    agg = DeviceAggregator(TorchModelAdapter(model, device="cuda:0", staging_capacity=30))
+    rng = np.random.default_rng(5)
+    agg.start_round(K)
+    acc = None
+    for k in range(K):
+        up = {n: rng.standard_normal(s, dtype=np.float32) for n, s in zip(names, shapes)}
+        agg.on_result({"client_id": k, "update_weight": up, "moving_loss": 1.0})
+        acc = fedavg_step(acc, up, k == 0)
+    want = fedavg_close(acc, K)
+    for got, w in zip(agg.model_wrapper.get_weights(), want):
+        np.testing.assert_array_equal(got.numpy(), w)
