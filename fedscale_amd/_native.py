@@ -19,6 +19,7 @@ FA_FINALIZE = 2
 FA_YOGI_INIT = 4
 FA_DP_WRITE_PARAM = 1
 FA_DP_SCALE_ONLY = 2
+FA_DT_F32, FA_DT_F64, FA_DT_I64 = 0, 1, 2
 
 
 class FedAggError(RuntimeError):
@@ -56,6 +57,15 @@ SIGNATURES = {
     "fa_pickle_strip": (_i64, [_c_void_p, _i64, _i64, _c_void_p, _i64, _c_void_p, _i32, _c_void_p]),
     "fa_prefix_box_combine": (_i32, [_c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _i32,
                                      _c_void_p, _c_void_p]),
+    "fa_sum_rows_f64": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p]),
+    # shard group (RCCL over the GPUs of this process; tables are host arrays of device pointers / streams)
+    "fa_rccl_available": (_i32, []),
+    "fa_rccl_init": (_i32, [_i32, _c_void_p, ctypes.POINTER(_c_void_p)]),
+    "fa_rccl_destroy": (_i32, [_c_void_p]),
+    "fa_rccl_all_gather": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i64, _i32, _c_void_p]),
+    "fa_rccl_all_reduce": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i64, _i32, _c_void_p]),
+    "fa_rccl_gather": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i64, _i32, _i32, _c_void_p]),
+    "fa_rccl_broadcast": (_i32, [_c_void_p, _c_void_p, _i64, _i32, _i32, _c_void_p]),
     # include/fedclient.h (client-side handlers; pointer tables are host arrays)
     "fa_prox_update": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _f32, _c_void_p]),
     "fa_sgd_prox_step": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _f32, _f32, _f64,

@@ -195,6 +195,27 @@ class BucketLayout:
         return out
 
 
+class HostRow:
+    """One arriving update gathered ONCE into pinned host rows covering the whole model: ``f`` the fp32
+    bucket (length >= P_full), ``i`` the side table.  A model sharded over the devices of one process
+    hands the same row to every part's ``ClientStaging.put``: each part copies its slice [p0, p1) to its own
+    device, so an upload crosses PCIe once, split over the GPUs' links.  ``pending`` collects the events of
+    those copies; the row is rewritten only after all of them (``wait``)."""
+
+    __slots__ = ("f", "i", "f_np", "i_np", "pending")
+
+    def __init__(self, ld: int, ldq: int):
+        self.f = torch.zeros(ld, dtype=torch.float32).pin_memory()
+        self.i = torch.zeros(ldq, dtype=torch.int64).pin_memory()
+        self.f_np, self.i_np = self.f.numpy(), self.i.numpy()
+        self.pending = []
+
+    def wait(self):
+        for ev in self.pending:
+            ev.synchronize()
+        self.pending = []
+
+
 class ClientStaging:
     """Device staging area for up to ``capacity`` client updates of one round (chunk).
 
@@ -224,13 +245,10 @@ class ClientStaging:
         self.generation = 0  # bumped by every DeviceRound that takes the slots over
         self.x = torch.zeros(self.capacity, layout.ld, dtype=torch.float32, device=self.device)
         self.xi = torch.zeros(self.capacity, layout.ldq, dtype=torch.int64, device=self.device)
-        self._ring = []
-        for _ in range(ring):
-            hf = torch.zeros(layout.ld, dtype=torch.float32).pin_memory()
-            hi = torch.zeros(layout.ldq, dtype=torch.int64).pin_memory()
-            # pinned rows, event of the last H2D, pending job, numpy views of the rows, the row's own event
-            self._ring.append([hf, hi, None, None, hf.numpy(), hi.numpy(), torch.cuda.Event()])
+        self._ring = []  # pinned rows for host updates, allocated on the first one (a part of a sharded
+        self._ring_n = ring  # model is fed HostRows by its coordinator and never needs its own)
         self._next = 0
+        self._row_evs = {}  # id(HostRow) -> event of this part's last H2D out of that row
         self.async_ingress = async_ingress
         self._pool = None
         nbytes = self.capacity * (layout.ld * 4 + layout.ldq * 8)
@@ -264,6 +282,8 @@ class ClientStaging:
         return ev
 
     def put(self, slot: int, update):
+        if type(update) is HostRow:
+            return self._put_row(slot, update)
         lay = self.layout
         values = lay.values_of(update)
         on_dev = [isinstance(v, torch.Tensor) and v.device == self.device for v in values]
@@ -275,6 +295,12 @@ class ClientStaging:
         if self.bulk:
             self._put_bulk(slot, plan)
             return
+        if not self._ring:
+            for _ in range(self._ring_n):
+                hf = torch.zeros(lay.ld, dtype=torch.float32).pin_memory()
+                hi = torch.zeros(lay.ldq, dtype=torch.int64).pin_memory()
+                # pinned rows, event of the last H2D, pending job, numpy views of the rows, the row's own event
+                self._ring.append([hf, hi, None, None, hf.numpy(), hi.numpy(), torch.cuda.Event()])
         r = self._ring[self._next]
         if r[3] is not None:  # the job that last used this pinned row
             r[2] = r[3].result()
@@ -292,8 +318,27 @@ class ClientStaging:
             r[2] = self._copy_in(slot, plan, r, stream, True)
         self._next = (self._next + 1) % len(self._ring)
 
-    def _put_bulk(self, slot: int, plan):
+    def _put_row(self, slot: int, row: "HostRow"):
+        """An update already gathered into a pinned row of the whole model (``HostRow``): copy this part's
+        slice [p0, p1) and the side table to the device (one H2D on this device's stream and link)."""
         lay = self.layout
+        if self.bulk:
+            self._claim_bulk(slot)
+            self._hx_np[slot, :lay.P] = row.f_np[lay.p0:lay.p1]
+            if lay.Q:
+                self._hxi_np[slot, :lay.Q] = row.i_np[:lay.Q]
+            self._bulk_hi = slot + 1
+            return
+        self.x[slot, :lay.P].copy_(row.f[lay.p0:lay.p1], non_blocking=True)
+        if lay.Q:
+            self.xi[slot, :lay.Q].copy_(row.i[:lay.Q], non_blocking=True)
+        ev = self._row_evs.get(id(row))
+        if ev is None:
+            ev = self._row_evs[id(row)] = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self._dev_index))
+        row.pending.append(ev)
+
+    def _claim_bulk(self, slot: int):
         if self._bulk_busy:  # the mirror's previous H2D must finish before its rows are rewritten
             self._bulk_ev.synchronize()
             self._bulk_busy = False
@@ -301,6 +346,10 @@ class ClientStaging:
             self.drain()  # keep pending rows contiguous
         if self._bulk_hi == self._bulk_lo:
             self._bulk_lo = self._bulk_hi = slot
+
+    def _put_bulk(self, slot: int, plan):
+        lay = self.layout
+        self._claim_bulk(slot)
         lay.run_host_gather(plan, self._hx_np[slot], self._hxi_np[slot], workers=self.pack_workers)
         self._bulk_hi = slot + 1
 

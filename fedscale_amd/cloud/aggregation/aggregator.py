@@ -52,6 +52,8 @@ class DeviceAggregatorMixin:
     #: pickled bytes kept for past model versions' get_weights() lists (FedBuff's model_cache holds
     #: max_staleness + 1 of them, config_parser.py:123)
     device_egress_past_versions = 8
+    #: GPU ordinals to shard the model over inside this process (None: FEDAGG_DEVICES, else one GPU)
+    device_shards = None
 
     _device_round = None
 
@@ -63,13 +65,27 @@ class DeviceAggregatorMixin:
         return self.model_in_update == self.tasks_round
 
     def init_model(self):
-        """aggregator.py:198-211, re-wired onto the device adapter + device server optimizer."""
+        """aggregator.py:198-211, re-wired onto the device adapter + device server optimizer.  With
+        ``device_shards`` (or FEDAGG_DEVICES="0,1,...") naming more than one GPU, the model is sharded over
+        them inside this one process (``ShardedModelAdapter``)."""
         from .optimizers import TorchServerOptimizer
 
         super().init_model()
         model = self.model_wrapper.get_model()
-        self.model_wrapper = TorchModelAdapter(
-            model, optimizer=TorchServerOptimizer(self.args.gradient_policy, self.args, self.device))
+        opt = TorchServerOptimizer(self.args.gradient_policy, self.args, self.device)
+        devs = self.device_shards
+        if devs is None:
+            import os
+
+            env = os.environ.get("FEDAGG_DEVICES")
+            devs = [int(d) for d in env.split(",") if d.strip()] if env else None
+        if devs is not None and len(devs) > 1:
+            from ..internal.sharded_model_adapter import ShardedModelAdapter
+
+            self.model_wrapper = ShardedModelAdapter(model, optimizer=opt, devices=devs)
+        else:
+            self.model_wrapper = TorchModelAdapter(model, optimizer=opt,
+                                                   device=devs[0] if devs else None)
 
     def _wrapper(self) -> TorchModelAdapter:
         w = self.model_wrapper

@@ -35,6 +35,12 @@ class TorchServerOptimizer(object):
             self.gradient_controller = YoGi(eta=args.yogi_eta, tau=args.yogi_tau, beta=args.yogi_beta,
                                             beta2=args.yogi_beta2)
 
+    def for_shard(self, device) -> "TorchServerOptimizer":
+        """The optimizer of one shard of a model sharded over the GPUs of this process: same mode and the
+        same live ``args`` (optimizers.py:69 reads the learning rate at step time), its own YoGi state
+        (m_t / v_t of the shard's parameters, yogi.py:11-19)."""
+        return TorchServerOptimizer(self.mode, self.args, device)
+
     # ---------------------------------------------------------------------------------------------
     def _dev(self):
         d = self.device

@@ -83,6 +83,15 @@ class EgressHandle:
         return (list, (list(self.weights()),))
 
 
+class _HostSnapshot:
+    """Pinned host copy of one model version (fp32 bucket ``f``, side table ``s``) and its reader count."""
+
+    __slots__ = ("version", "f", "s", "readers")
+
+    def __init__(self, version, f, s):
+        self.version, self.f, self.s, self.readers = version, f, s, 0
+
+
 def _resolve_device(device) -> torch.device:
     if device is None:
         return torch.device("cuda", torch.cuda.current_device())
@@ -121,11 +130,21 @@ class TorchModelAdapter(ModelAdapterBase):
         self._pack_values(list(_load_from) if _load_from is not None else list(sd.values()), cur_f, cur_s)
         self._f[0].copy_(cur_f)
         self._s[0].copy_(cur_s.to(torch.int64))
+        self._ready = torch.cuda.Event()  # the kernels that wrote the current model buffers
+        self._init_egress(_load_from is None)
+
+    def _init_egress(self, module_in_sync: bool):
+        """Egress state, shared with the servicer threads (aggregator.py:177-178: 20 of them call
+        get_weights / serialize the model while the main thread applies rounds).  Host snapshots are
+        immutable per model version; the lock guards (version, current snapshot, cached bytes)."""
         self._version = 0  # bumps on every device-side model update
-        self._host_cache = None
+        self._egress_lock = threading.Lock()
+        self._pickle_lock = threading.Lock()  # one thread pickles a version; the others take its bytes
+        self._snap: Optional[_HostSnapshot] = None
+        self._snap_pool: list = []  # pinned buffers of retired snapshots no reader holds any more
         self._egress_cache = None
         self._egress_id = next(_EGRESS_IDS)
-        self._module_version = 0 if _load_from is None else -1
+        self._module_version = 0 if module_in_sync else -1
 
     # ---- internal buffers ---------------------------------------------------------------------
     def _snapshot(self) -> FlatState:
@@ -135,8 +154,10 @@ class TorchModelAdapter(ModelAdapterBase):
         return self._f[1 - self._cur], self._s[1 - self._cur]
 
     def _commit_scratch(self):
-        self._cur = 1 - self._cur
-        self._version += 1
+        self._ready.record(torch.cuda.current_stream(self.device))
+        with self._egress_lock:  # (buffer, version) flip atomically for the servicer threads
+            self._cur = 1 - self._cur
+            self._version += 1
 
     def _sqnorm_allreduce(self):
         return self.shards.all_reduce_sum if self.shards.shards_params else None
@@ -177,19 +198,43 @@ class TorchModelAdapter(ModelAdapterBase):
         ns.copy_(cur_s.to(torch.float32).to(torch.int64))  # float32 -> int64 load truncates (:31-35)
         self._commit_scratch()
 
-    def _host_copy(self):
-        """One D2H (after the shard all-gather) per model version, cached for every egress request of the
-        round (the reference clones + pickles per executor request, aggregator.py:788-804, 902-909)."""
-        if self._host_cache is None or self._host_cache[0] != self._version:
-            L = self.layout
-            full = self.shards.all_gather(self._f[self._cur])
-            # one pinned buffer, reused across versions: every consumer clones out of it
-            f_cpu = self._host_cache[1] if self._host_cache is not None else (
-                torch.empty(L.P_full, dtype=torch.float32, pin_memory=True))
-            f_cpu.copy_(full[:L.P_full])
-            s_cpu = self._s[self._cur][:L.Q].to("cpu")
-            self._host_cache = (self._version, f_cpu, s_cpu)
-        return self._host_cache[1], self._host_cache[2]
+    def _copy_to_host(self, f_cpu: torch.Tensor, s_cpu: torch.Tensor):
+        """D2H of the current model into pinned f_cpu[:P_full] / s_cpu[:Q] (the caller holds the egress
+        lock, so no round commits meanwhile; synchronous).  Parameter-sharded SPMD ranks all-gather
+        first: every rank must then call egress from its main thread, in step (bench / tests)."""
+        L = self.layout
+        self._ready.synchronize()
+        full = self.shards.all_gather(self._f[self._cur])
+        f_cpu[:L.P_full].copy_(full[:L.P_full])
+        s_cpu[:L.Q].copy_(self._s[self._cur][:L.Q])
+
+    def _acquire_host(self) -> "_HostSnapshot":
+        """The host snapshot of the current model version (one D2H per version), held by the caller until
+        ``_release_host``: a later version goes to another pinned buffer, so readers of this one never see
+        it change (aggregator.py:788-804, 902-909 read the model from up to 20 servicer threads)."""
+        with self._egress_lock:
+            snap = self._snap
+            if snap is None or snap.version != self._version:
+                L = self.layout
+                f = self._snap_pool.pop() if self._snap_pool else torch.empty(max(1, L.P_full), dtype=torch.float32,
+                                                                              pin_memory=True)
+                s_cpu = torch.empty(max(1, L.Q), dtype=torch.int64)
+                self._copy_to_host(f, s_cpu)
+                old, snap = snap, _HostSnapshot(self._version, f, s_cpu)
+                self._snap = snap
+                if old is not None and old.readers == 0:
+                    self._snap_pool.append(old.f)
+            snap.readers += 1
+            return snap
+
+    def _release_host(self, snap: "_HostSnapshot"):
+        with self._egress_lock:
+            snap.readers -= 1
+            if snap.readers == 0 and snap is not self._snap:
+                self._snap_pool.append(snap.f)
+
+    def _clone_weights(self, snap: "_HostSnapshot") -> list:
+        return [t.clone() for t in self.layout.unpack(snap.f, snap.s)]
 
     def get_weights(self) -> List[torch.Tensor]:
         """torch_model_adapter.py:41-47: cloned CPU tensors in state_dict order (gathers the shards).
@@ -200,29 +245,53 @@ class TorchModelAdapter(ModelAdapterBase):
         if getattr(_HANDLE_ONCE, "adapter", None) is self:  # the caller only serialises this list
             _HANDLE_ONCE.adapter = None
             return self.egress_handle()
-        f_cpu, s_cpu = self._host_copy()
-        out = EgressWeights(t.clone() for t in self.layout.unpack(f_cpu, s_cpu))
-        out.egress_key = (self._egress_id, self._version)
+        snap = self._acquire_host()
+        try:
+            out = EgressWeights(self._clone_weights(snap))
+            out.egress_key = (self._egress_id, snap.version)
+        finally:
+            self._release_host(snap)
         return out
 
     def egress_bytes(self, key) -> Optional[bytes]:
         """``pickle.dumps`` of get_weights() for model version ``key`` — the bytes the reference's
         serialize_response makes per executor request (aggregator.py:788-804, 902-909) — made once per
-        model version from the adapter's own host copy.  None when ``key`` is not the current version."""
+        model version from the adapter's own host copy.  None when ``key`` is not the current version.
+        Thread-safe: the bytes always belong to exactly the version of ``key``."""
         import pickle
 
-        if key != (self._egress_id, self._version):
-            return None
-        if self._egress_cache is None or self._egress_cache[0] != key:
-            f_cpu, s_cpu = self._host_copy()
-            self._egress_cache = None
-            self._egress_cache = (key, pickle.dumps([t.clone() for t in self.layout.unpack(f_cpu, s_cpu)]))
-        return self._egress_cache[1]
+        with self._egress_lock:
+            if key != (self._egress_id, self._version):
+                return None
+            c = self._egress_cache
+            if c is not None and c[0] == key:
+                return c[1]
+        with self._pickle_lock:  # one thread pickles; the others wait and take its bytes
+            with self._egress_lock:
+                c = self._egress_cache
+                if c is not None and c[0] == key:
+                    return c[1]
+            snap = self._acquire_host()
+            try:
+                if (self._egress_id, snap.version) != key:
+                    return None  # a round committed meanwhile: the caller's list is of an older version
+                b = pickle.dumps(self._clone_weights(snap))
+            finally:
+                self._release_host(snap)
+            with self._egress_lock:
+                c = self._egress_cache
+                if c is None or c[0][1] < key[1]:
+                    self._egress_cache = (key, b)
+            return b
 
     def egress_handle(self) -> EgressHandle:
         """``get_weights()`` for a caller that only serialises it: no clone (``EgressHandle``)."""
-        key = (self._egress_id, self._version)
-        return EgressHandle(key, self.egress_bytes(key))
+        while True:
+            with self._egress_lock:
+                key = (self._egress_id, self._version)
+            b = self.egress_bytes(key)
+            if b is not None:  # else a round committed between the two lines: take the new version
+                return EgressHandle(key, b)
 
     def handle_next_get_weights(self):
         """Context: the next get_weights() on this thread returns ``egress_handle()`` (no clone). For a
@@ -280,9 +349,12 @@ class TorchModelAdapter(ModelAdapterBase):
         if rnd.policy == "qfedavg":
             if mode != "q-fedavg":
                 raise RuntimeError("a q-FedAvg round needs the q-fedavg server optimizer")
-            rnd.finalize_qfed(out=out_f, model_side=out_s, sqnorm_allreduce=self._sqnorm_allreduce())
-            self._mean_valid = False
-            self._mean_round = rnd  # the mean can still be recomputed lazily from the staged updates
+            rnd.qfed_fold()
+            allreduce = self._sqnorm_allreduce()
+            if allreduce is not None and rnd.cg is None:
+                allreduce(rnd.sqnorm)
+            self._finish_qfed(rnd)
+            return
         elif mode == "fed-yogi":
             y = opt.gradient_controller
             y.bind(L, self.device)
@@ -305,12 +377,34 @@ class TorchModelAdapter(ModelAdapterBase):
             self._mean_valid = True
         self._commit_scratch()
 
+    def _finish_qfed(self, rnd: DeviceRound):
+        """hs + step of a folded q-FedAvg round (its norms already summed over the shards), then commit."""
+        out_f, out_s = self._scratch_buffers()
+        rnd.qfed_finish(out=out_f, model_side=out_s)
+        self._mean_valid = False
+        self._mean_round = rnd  # the mean can still be recomputed lazily from the staged updates
+        self._commit_scratch()
+
     def round_mean_weights(self):
         """The reference's Aggregator.model_weights after the last result of a round (the FedAvg mean,
         aggregator.py:505-507): fp32 entries float32, int64 entries float64 — materialised lazily."""
         return LazyWeights(self)
 
     def _fetch_mean(self) -> list:
+        mean_f, mean_s = self._mean_device()
+        L = self.layout
+        full = self.shards.all_gather(mean_f[:L.ld])
+        return self._mean_lists(full[:L.P_full].to("cpu").numpy(), mean_s[:L.Q].to("cpu").numpy())
+
+    def _mean_lists(self, f_cpu, s_cpu) -> list:
+        out = []
+        for e in self.layout.entries:
+            src = f_cpu if e.kind == "f" else s_cpu
+            out.append(np.array(src[e.offset:e.offset + e.numel].reshape(e.shape)))
+        return out
+
+    def _mean_device(self):
+        """(fp32 mean slice, float64 side mean) of the last round on this device."""
         rnd = getattr(self, "_mean_round", None)
         if not self._mean_valid and rnd is not None:
             L = self.layout
@@ -322,15 +416,7 @@ class TorchModelAdapter(ModelAdapterBase):
             raise RuntimeError("the FedAvg mean of this round is not available on the device: a q-FedAvg "
                                "round keeps it only while all K updates are still staged (one chunk), and "
                                "fed-yogi keeps it unless keep_mean=False")
-        L = self.layout
-        full = self.shards.all_gather(self._mean_f[:L.ld])
-        f_cpu = full[:L.P_full].to("cpu").numpy()
-        s_cpu = self._mean_s[:L.Q].to("cpu").numpy()
-        out = []
-        for e in L.entries:
-            src = f_cpu if e.kind == "f" else s_cpu
-            out.append(np.array(src[e.offset:e.offset + e.numel].reshape(e.shape)))
-        return out
+        return self._mean_f, self._mean_s
 
 
 class LazyWeights:

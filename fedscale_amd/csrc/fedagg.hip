@@ -870,6 +870,23 @@ extern "C" int fa_qfed_finalize(const float* last, const float* delta, const flo
   return check_launch("fa_qfed_finalize");
 }
 
+// fixed-order sum of per-shard fp64 rows (after an all-gather of the shards' partial norms)
+__global__ __launch_bounds__(256) void k_sum_rows_f64(const double* __restrict__ x, int64_t ld, int n, int64_t K,
+                                                     double* out) {
+  for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < K; k += (int64_t)gridDim.x * 256) {
+    double s = x[k];
+    for (int r = 1; r < n; ++r) s += x[(int64_t)r * ld + k];
+    out[k] = s;
+  }
+}
+
+extern "C" int fa_sum_rows_f64(const double* x, int64_t ld, int32_t n, int64_t K, double* out, fa_stream_t stream) {
+  if (n < 1 || K < 0 || ld < K || !x || !out) return fail(FA_E_ARG, "fa_sum_rows_f64: bad arguments");
+  if (K == 0) return FA_OK;
+  hipLaunchKernelGGL(k_sum_rows_f64, dim3(stride_grid(K)), dim3(256), 0, (hipStream_t)stream, x, ld, (int)n, K, out);
+  return check_launch("fa_sum_rows_f64");
+}
+
 // ------------------------------------------------------------------------------------------------
 // side table (int64 state_dict entries): one thread per element, clients in arrival order
 // ------------------------------------------------------------------------------------------------

@@ -1,0 +1,220 @@
+// rccl_comm.cpp — RCCL collectives over the GPUs one aggregator process drives (include/fedagg.h,
+// "shard group" section).
+//
+// FedScale's aggregator is ONE process: every upload lands in it (aggregator.py:919-963) and egress is
+// served from its gRPC servicer threads (aggregator.py:871-917).  To spread a round over the node's GPUs
+// behind that unmodified event loop, the library drives N devices from the one process and the
+// cross-device steps are RCCL collectives over xGMI issued for all N devices at once
+// (ncclCommInitAll + ncclGroupStart/End, one stream per device).  No rendezvous, no second process.
+//
+// RCCL is resolved at run time (dlopen): the copy torch already loaded is reused when present, so one
+// RCCL lives in the process; the library itself has no link-time dependency on it and loads on hosts
+// without RCCL (fa_rccl_available() then returns 0 and fa_rccl_init fails with FA_E_HIP).
+#include <dlfcn.h>
+#include <stdint.h>
+#include <stdio.h>
+
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include <rccl/rccl.h>
+
+#include "../../include/fedagg.h"
+
+extern "C" __attribute__((visibility("hidden"))) int fa_internal_set_error(int code, const char* msg);
+
+namespace {
+
+struct RcclApi {
+  decltype(&ncclCommInitAll) init_all = nullptr;
+  decltype(&ncclCommDestroy) destroy = nullptr;
+  decltype(&ncclGroupStart) group_start = nullptr;
+  decltype(&ncclGroupEnd) group_end = nullptr;
+  decltype(&ncclAllGather) all_gather = nullptr;
+  decltype(&ncclAllReduce) all_reduce = nullptr;
+  decltype(&ncclGather) gather = nullptr;
+  decltype(&ncclBroadcast) broadcast = nullptr;
+  decltype(&ncclGetErrorString) error_string = nullptr;
+  decltype(&ncclGetVersion) version = nullptr;
+  bool ok = false;
+};
+
+RcclApi g_api;
+std::once_flag g_api_once;
+
+void load_api() {
+  // the RCCL torch loaded (soname librccl.so.1) first; else the ROCm install's
+  void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+  if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+  if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+  if (!h) return;
+#define FA_SYM(field, name) g_api.field = reinterpret_cast<decltype(g_api.field)>(dlsym(h, name))
+  FA_SYM(init_all, "ncclCommInitAll");
+  FA_SYM(destroy, "ncclCommDestroy");
+  FA_SYM(group_start, "ncclGroupStart");
+  FA_SYM(group_end, "ncclGroupEnd");
+  FA_SYM(all_gather, "ncclAllGather");
+  FA_SYM(all_reduce, "ncclAllReduce");
+  FA_SYM(gather, "ncclGather");
+  FA_SYM(broadcast, "ncclBroadcast");
+  FA_SYM(error_string, "ncclGetErrorString");
+  FA_SYM(version, "ncclGetVersion");
+#undef FA_SYM
+  g_api.ok = g_api.init_all && g_api.destroy && g_api.group_start && g_api.group_end && g_api.all_gather &&
+             g_api.all_reduce && g_api.gather && g_api.broadcast && g_api.error_string;
+}
+
+const RcclApi* api() {
+  std::call_once(g_api_once, load_api);
+  return g_api.ok ? &g_api : nullptr;
+}
+
+struct Comm {
+  int n = 0;
+  std::vector<ncclComm_t> comms;
+};
+
+int err(int code, const char* what, ncclResult_t r) {
+  char buf[256];
+  const RcclApi* a = api();
+  snprintf(buf, sizeof(buf), "%s: %s", what, a ? a->error_string(r) : "RCCL unavailable");
+  return fa_internal_set_error(code, buf);
+}
+
+int dtype_of(int32_t dt, ncclDataType_t* out, size_t* elem) {
+  switch (dt) {
+    case FA_DT_F32: *out = ncclFloat32; *elem = 4; return FA_OK;
+    case FA_DT_F64: *out = ncclFloat64; *elem = 8; return FA_OK;
+    case FA_DT_I64: *out = ncclInt64; *elem = 8; return FA_OK;
+    default: return fa_internal_set_error(FA_E_ARG, "fa_rccl: unknown dtype");
+  }
+}
+
+int check(void* comm, int64_t count, const char* what, Comm** c) {
+  if (!api()) return fa_internal_set_error(FA_E_HIP, "fa_rccl: RCCL could not be loaded");
+  if (!comm || count < 0) return fa_internal_set_error(FA_E_ARG, what);
+  *c = static_cast<Comm*>(comm);
+  return FA_OK;
+}
+
+// one grouped launch: op(i) issues device i's part of the collective
+template <class F>
+int grouped(const Comm* c, const char* what, F op) {
+  const RcclApi* a = api();
+  ncclResult_t r = a->group_start();
+  if (r != ncclSuccess) return err(FA_E_HIP, what, r);
+  ncclResult_t first = ncclSuccess;
+  for (int i = 0; i < c->n; ++i) {
+    r = op(i);
+    if (r != ncclSuccess && first == ncclSuccess) first = r;
+  }
+  r = a->group_end();  // always close the group, even after a failed enqueue
+  if (first != ncclSuccess) return err(FA_E_HIP, what, first);
+  if (r != ncclSuccess) return err(FA_E_HIP, what, r);
+  return FA_OK;
+}
+
+}  // namespace
+
+extern "C" int fa_rccl_available(void) { return api() ? 1 : 0; }
+
+extern "C" int fa_rccl_init(int32_t ndev, const int32_t* devs, void** comm_out) {
+  if (ndev < 1 || !devs || !comm_out) return fa_internal_set_error(FA_E_ARG, "fa_rccl_init: bad arguments");
+  for (int i = 0; i < ndev; ++i)
+    for (int j = 0; j < i; ++j)
+      if (devs[i] == devs[j])
+        return fa_internal_set_error(FA_E_ARG, "fa_rccl_init: a device appears twice (one rank per GPU)");
+  const RcclApi* a = api();
+  if (!a) return fa_internal_set_error(FA_E_HIP, "fa_rccl_init: RCCL could not be loaded");
+  Comm* c = new (std::nothrow) Comm();
+  if (!c) return fa_internal_set_error(FA_E_HIP, "fa_rccl_init: out of memory");
+  c->n = ndev;
+  c->comms.resize(ndev);
+  std::vector<int> d(devs, devs + ndev);
+  ncclResult_t r = a->init_all(c->comms.data(), ndev, d.data());
+  if (r != ncclSuccess) {
+    delete c;
+    return err(FA_E_HIP, "fa_rccl_init: ncclCommInitAll", r);
+  }
+  *comm_out = c;
+  return FA_OK;
+}
+
+extern "C" int fa_rccl_destroy(void* comm) {
+  if (!comm) return FA_OK;
+  Comm* c = static_cast<Comm*>(comm);
+  const RcclApi* a = api();
+  int rc = FA_OK;
+  if (a)
+    for (ncclComm_t x : c->comms) {
+      ncclResult_t r = a->destroy(x);
+      if (r != ncclSuccess && rc == FA_OK) rc = err(FA_E_HIP, "fa_rccl_destroy", r);
+    }
+  delete c;
+  return rc;
+}
+
+extern "C" int fa_rccl_all_gather(void* comm, const void* const* send, void* const* recv, int64_t count,
+                                  int32_t dtype, void* const* streams) {
+  Comm* c;
+  int e = check(comm, count, "fa_rccl_all_gather: bad arguments", &c);
+  if (e) return e;
+  ncclDataType_t dt;
+  size_t sz;
+  if ((e = dtype_of(dtype, &dt, &sz))) return e;
+  if (!send || !recv || !streams) return fa_internal_set_error(FA_E_ARG, "fa_rccl_all_gather: NULL table");
+  const RcclApi* a = api();
+  return grouped(c, "fa_rccl_all_gather", [&](int i) {
+    return a->all_gather(send[i], recv[i], (size_t)count, dt, c->comms[i], (hipStream_t)streams[i]);
+  });
+}
+
+extern "C" int fa_rccl_all_reduce(void* comm, const void* const* send, void* const* recv, int64_t count,
+                                  int32_t dtype, void* const* streams) {
+  Comm* c;
+  int e = check(comm, count, "fa_rccl_all_reduce: bad arguments", &c);
+  if (e) return e;
+  ncclDataType_t dt;
+  size_t sz;
+  if ((e = dtype_of(dtype, &dt, &sz))) return e;
+  if (!send || !recv || !streams) return fa_internal_set_error(FA_E_ARG, "fa_rccl_all_reduce: NULL table");
+  const RcclApi* a = api();
+  return grouped(c, "fa_rccl_all_reduce", [&](int i) {
+    return a->all_reduce(send[i], recv[i], (size_t)count, dt, ncclSum, c->comms[i], (hipStream_t)streams[i]);
+  });
+}
+
+extern "C" int fa_rccl_gather(void* comm, const void* const* send, void* recv_root, int64_t count, int32_t dtype,
+                              int32_t root, void* const* streams) {
+  Comm* c;
+  int e = check(comm, count, "fa_rccl_gather: bad arguments", &c);
+  if (e) return e;
+  ncclDataType_t dt;
+  size_t sz;
+  if ((e = dtype_of(dtype, &dt, &sz))) return e;
+  if (!send || !recv_root || !streams || root < 0 || root >= c->n)
+    return fa_internal_set_error(FA_E_ARG, "fa_rccl_gather: bad root or NULL table");
+  const RcclApi* a = api();
+  return grouped(c, "fa_rccl_gather", [&](int i) {
+    return a->gather(send[i], i == root ? recv_root : nullptr, (size_t)count, dt, root, c->comms[i],
+                     (hipStream_t)streams[i]);
+  });
+}
+
+extern "C" int fa_rccl_broadcast(void* comm, void* const* bufs, int64_t count, int32_t dtype, int32_t root,
+                                 void* const* streams) {
+  Comm* c;
+  int e = check(comm, count, "fa_rccl_broadcast: bad arguments", &c);
+  if (e) return e;
+  ncclDataType_t dt;
+  size_t sz;
+  if ((e = dtype_of(dtype, &dt, &sz))) return e;
+  if (!bufs || !streams || root < 0 || root >= c->n)
+    return fa_internal_set_error(FA_E_ARG, "fa_rccl_broadcast: bad root or NULL table");
+  const RcclApi* a = api();
+  return grouped(c, "fa_rccl_broadcast", [&](int i) {
+    return a->broadcast(bufs[i], bufs[i], (size_t)count, dt, root, c->comms[i], (hipStream_t)streams[i]);
+  });
+}

@@ -126,6 +126,19 @@ def qfed_finalize(last, delta, hs, out, P):
     call("fa_qfed_finalize", ptr(last), ptr(delta), ptr(hs), ptr(out), P, _stream(out))
 
 
+def sum_rows_f64(x: torch.Tensor, out: torch.Tensor):
+    """out[k] = fixed-order sum over the rows of x[n, K] (fa_sum_rows_f64); out may alias x[0]."""
+    _dev(x, torch.float64, "x", align=8)
+    if x.dim() != 2:
+        raise ValueError("x: expected [n, K]")
+    n, K = x.shape
+    _dev(out, torch.float64, "out", K, align=8)
+    if out.device != x.device:
+        raise ValueError("out and x must be on the same device")
+    call("fa_sum_rows_f64", ptr(x), K, n, K, ptr(out), _stream(out))
+    return out
+
+
 # ---- side table (int64 entries) ---------------------------------------------------------------
 def side_accumulate(xi, K, Q, mode, *, w=None, acc_i=None, acc_d=None, accumulate=False):
     if Q == 0 or K == 0:

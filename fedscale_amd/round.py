@@ -230,16 +230,25 @@ class DeviceRound:
 
         ``sqnorm_allreduce(t)`` sums the per-client partial squared norms across shards (RCCL) when the
         model is sharded over ranks; the side table contributes once, after the all-reduce."""
+        self.qfed_fold()
+        if self.cg is None and sqnorm_allreduce is not None:
+            sqnorm_allreduce(self.sqnorm)
+        self.qfed_finish(out=out, model_side=model_side)
+
+    def qfed_fold(self):
+        """Phase 1 of the finish: fold the last chunk.  ``sqnorm`` then holds this shard's partial per-client
+        squared norms (the fp32 bucket part; summed over the shards by the caller between the phases)."""
         self._check_complete()
-        L = self.layout
         if self.slot:
             self._fold_chunk()
         if self.cg is not None:
             # each client's norms were computed on its owner rank only: the sum is a gather (exact);
             # delta and delta_s are per-rank partial chains
             self._cross_rank_sum(self.delta, self.delta_s, self.sqnorm, self.sqnorm_side)
-        elif sqnorm_allreduce is not None:
-            sqnorm_allreduce(self.sqnorm)
+
+    def qfed_finish(self, *, out: torch.Tensor, model_side: torch.Tensor):
+        """Phase 2: hs over the (shard-summed) norms and the step."""
+        L = self.layout
         # side table: replicated on every rank, so it is added once, after the cross-shard sum
         self.sqnorm += self.sqnorm_side
         c1 = torch.from_numpy(self.c1).to(self.device, non_blocking=True)

@@ -83,22 +83,16 @@ class ShardGroup:
         model is replicated, so the local copy already is the whole model."""
         if not self.shards_params:
             return shard
-        import torch.distributed as dist
-
-        if self._host_staged(shard):
-            return self.__class__.all_gather(self, shard.cpu()).to(shard.device)
-        out = torch.empty(self.world * shard.numel(), dtype=shard.dtype, device=shard.device)
-        if shard.device.type == "cpu" and dist.get_backend(self.group) == "gloo":
-            parts = list(out.chunk(self.world))
-            dist.all_gather(parts, shard.contiguous(), group=self.group)
-            return torch.cat(parts)
-        dist.all_gather_into_tensor(out, shard.contiguous(), group=self.group)
-        return out
+        return self.collective_all_gather(shard)
 
     def all_reduce_sum(self, t: torch.Tensor) -> torch.Tensor:
         """In-place sum over ranks (RCCL all-reduce; the K per-client partial norms of q-FedAvg)."""
         if self.world == 1:
             return t
+        return self.collective_all_reduce(t)
+
+    # raw collectives (no world-1 short cut): what the wrappers above issue, callable at any world size
+    def collective_all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         import torch.distributed as dist
 
         if self._host_staged(t):
@@ -108,3 +102,164 @@ class ShardGroup:
             return t
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
         return t
+
+    def collective_all_gather(self, shard: torch.Tensor) -> torch.Tensor:
+        import torch.distributed as dist
+
+        world = dist.get_world_size(self.group)
+        if self._host_staged(shard):
+            return self.collective_all_gather(shard.cpu()).to(shard.device)
+        out = torch.empty(world * shard.numel(), dtype=shard.dtype, device=shard.device)
+        if shard.device.type == "cpu":
+            parts = list(out.chunk(world))
+            dist.all_gather(parts, shard.contiguous(), group=self.group)
+            return torch.cat(parts)
+        dist.all_gather_into_tensor(out, shard.contiguous(), group=self.group)
+        return out
+
+
+class PartOf(ShardGroup):
+    """Part r of N of a model sharded over the devices of ONE process (``DeviceGroup``): the shard
+    geometry of rank r of N, but no process-group collectives — the cross-part steps are issued by the
+    coordinating ``ShardedModelAdapter`` for all parts at once."""
+
+    def __init__(self, rank: int, world: int, devices: "DeviceGroup"):
+        super().__init__(rank, world, None, "params")
+        self.devices = devices
+
+    def all_gather(self, shard):
+        raise RuntimeError("in-process shard: the coordinating adapter reassembles the parts")
+
+    def all_reduce_sum(self, t):
+        raise RuntimeError("in-process shard: the coordinating adapter combines the parts")
+
+
+class DeviceGroup:
+    """The GPUs ONE aggregator process drives (FedScale's aggregator is a single process, aggregator.py:
+    177-192, 919-963).  Cross-device steps are RCCL collectives over xGMI issued for every device at once
+    from the calling thread (``fa_rccl_*``, one communicator for the group); when a device appears more
+    than once (several shards on one card, as in tests) or RCCL is unavailable, the same steps run as
+    device-to-device copies.  Either way the combination order is fixed (all-gather, then a fixed-order
+    sum), so the result does not depend on the transport.
+
+    ``transport``: "rccl", "copy" or None (choose: RCCL whenever the devices are distinct)."""
+
+    def __init__(self, devices, transport: Optional[str] = None):
+        devs = [torch.device(d) if not isinstance(d, int) else torch.device("cuda", d) for d in devices]
+        if not devs:
+            raise ValueError("DeviceGroup needs at least one device")
+        for d in devs:
+            if d.type != "cuda" or d.index is None:
+                raise ValueError(f"device {d}: a DeviceGroup holds indexed GPUs (cuda:N); no CPU fallback")
+        self.devices = devs
+        self.world = len(devs)
+        distinct = len({d.index for d in devs}) == len(devs)
+        if transport is None:
+            from . import _native
+
+            transport = "rccl" if distinct and _native.load().fa_rccl_available() else "copy"
+        if transport not in ("rccl", "copy"):
+            raise ValueError(f"transport {transport!r}")
+        if transport == "rccl" and not distinct:
+            raise ValueError("RCCL needs one shard per GPU (a device appears twice)")
+        self.transport = transport
+        self._comm = None
+
+    # ---- RCCL communicator ------------------------------------------------------------------------
+    def _rccl(self):
+        if self._comm is None:
+            import ctypes
+
+            from . import _native
+
+            devs = (ctypes.c_int32 * self.world)(*[d.index for d in self.devices])
+            h = ctypes.c_void_p()
+            _native.call("fa_rccl_init", self.world, devs, ctypes.byref(h))
+            self._comm = h
+        return self._comm
+
+    def close(self):
+        if self._comm is not None:
+            from . import _native
+
+            comm, self._comm = self._comm, None
+            _native.call("fa_rccl_destroy", comm)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _tables(self, *lists):
+        import ctypes
+
+        out = []
+        for lst in lists:
+            out.append((ctypes.c_void_p * self.world)(*[None if t is None else t.data_ptr() for t in lst]))
+        streams = (ctypes.c_void_p * self.world)(*[torch.cuda.current_stream(d).cuda_stream for d in self.devices])
+        return out, streams
+
+    @staticmethod
+    def _dt(t: torch.Tensor) -> int:
+        from . import _native
+
+        return {torch.float32: _native.FA_DT_F32, torch.float64: _native.FA_DT_F64,
+                torch.int64: _native.FA_DT_I64}[t.dtype]
+
+    # ---- collectives over the parts ---------------------------------------------------------------
+    def all_gather(self, parts, outs):
+        """outs[i][r*n:(r+1)*n] = parts[r] for every part i (n = parts[r].numel(), equal for all r)."""
+        n = parts[0].numel()
+        if self.transport == "rccl":
+            from . import _native
+
+            (send, recv), streams = self._tables(parts, outs)
+            _native.call("fa_rccl_all_gather", self._rccl(), send, recv, n, self._dt(parts[0]), streams)
+            return outs
+        for i, o in enumerate(outs):
+            for r, p in enumerate(parts):
+                o[r * n:(r + 1) * n].copy_(p.reshape(-1), non_blocking=True)
+        return outs
+
+    def gather(self, parts, out_root, root: int = 0):
+        """out_root[r*n:(r+1)*n] = parts[r], on device ``root``."""
+        n = parts[0].numel()
+        if self.transport == "rccl":
+            import ctypes
+
+            from . import _native
+
+            (send,), streams = self._tables(parts)
+            _native.call("fa_rccl_gather", self._rccl(), send, ctypes.c_void_p(out_root.data_ptr()), n,
+                         self._dt(parts[0]), root, streams)
+            return out_root
+        for r, p in enumerate(parts):
+            out_root[r * n:(r + 1) * n].copy_(p.reshape(-1), non_blocking=True)
+        return out_root
+
+    def broadcast(self, bufs, root: int = 0):
+        """bufs[i] <- bufs[root] for every part i."""
+        n = bufs[root].numel()
+        if self.transport == "rccl":
+            from . import _native
+
+            (b,), streams = self._tables(bufs)
+            _native.call("fa_rccl_broadcast", self._rccl(), b, n, self._dt(bufs[root]), root, streams)
+            return bufs
+        for i, t in enumerate(bufs):
+            if i != root:
+                t.copy_(bufs[root], non_blocking=True)
+        return bufs
+
+    def sum_f64(self, parts, scratch=None):
+        """parts[i] <- ((parts[0] + parts[1]) + ...) on every device: per-shard fp64 partials (q-FedAvg's
+        per-client squared norms), combined by an all-gather and a fixed-order sum (fa_sum_rows_f64)."""
+        from . import kernels as kx
+
+        n = parts[0].numel()
+        outs = scratch or [torch.empty(self.world * n, dtype=torch.float64, device=p.device) for p in parts]
+        self.all_gather(parts, outs)
+        for p, o in zip(parts, outs):
+            kx.sum_rows_f64(o.view(self.world, n), p)
+        return parts

@@ -189,6 +189,45 @@ int fa_host_gather(void* dst, const void* const* srcs, const int64_t* dst_off, c
 int64_t fa_pickle_strip(const uint8_t* in, int64_t n, int64_t min_bytes, uint8_t* out, int64_t out_cap,
                         int64_t* regions, int32_t max_regions, int32_t* nregions);
 
+/*
+ * Fixed-order sum of n rows of K fp64 values: out[k] = ((x[0][k] + x[1][k]) + x[2][k]) + ...  (row
+ * stride ld).  Combines per-shard partial q-FedAvg squared norms (optimizers.py:96-97 summed over the
+ * model's shards) after an all-gather, so the result does not depend on the collective's internal
+ * order or on the transport.  out may alias x[0].
+ */
+int fa_sum_rows_f64(const double* x, int64_t ld, int32_t n, int64_t K, double* out, fa_stream_t stream);
+
+/*
+ * Shard group: RCCL collectives over the N GPUs that ONE aggregator process drives.
+ *
+ * Replaces nothing in the reference (its aggregator is one process on one device, aggregator.py:177-192,
+ * 919-963); this is what lets the drop-in spread a round over a node's GPUs behind that unmodified
+ * single-process event loop: the parameter shards (or client blocks) live on N devices of the one
+ * process, and the cross-device steps are RCCL collectives over xGMI, issued for all N devices in one
+ * ncclGroupStart/End from the calling thread.  RCCL is loaded at run time (the copy torch already
+ * loaded is reused); fa_rccl_available() == 0 when it cannot be found.
+ *
+ * Tables (send / recv / bufs / streams) are HOST arrays of N device pointers / hipStream_t, indexed by
+ * the position in `devs` given to fa_rccl_init.  count is in elements of `dtype` per device.
+ *   fa_rccl_init       ncclCommInitAll over devs[0..ndev) (distinct device ordinals)
+ *   fa_rccl_all_gather recv[i][r*count + j] = send[r][j]
+ *   fa_rccl_all_reduce recv[i][j] = sum_r send[r][j]
+ *   fa_rccl_gather     recv_root[r*count + j] = send[r][j]  (on device `root` only)
+ *   fa_rccl_broadcast  bufs[i][j] = bufs[root][j]
+ */
+enum { FA_DT_F32 = 0, FA_DT_F64 = 1, FA_DT_I64 = 2 };
+int fa_rccl_available(void);
+int fa_rccl_init(int32_t ndev, const int32_t* devs, void** comm_out);
+int fa_rccl_destroy(void* comm);
+int fa_rccl_all_gather(void* comm, const void* const* send, void* const* recv, int64_t count, int32_t dtype,
+                       void* const* streams);
+int fa_rccl_all_reduce(void* comm, const void* const* send, void* const* recv, int64_t count, int32_t dtype,
+                       void* const* streams);
+int fa_rccl_gather(void* comm, const void* const* send, void* recv_root, int64_t count, int32_t dtype, int32_t root,
+                   void* const* streams);
+int fa_rccl_broadcast(void* comm, void* const* bufs, int64_t count, int32_t dtype, int32_t root,
+                      void* const* streams);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,357 @@
+"""Multi-GPU behind the reference's single-process aggregator (``ShardedModelAdapter``).
+
+The box these run on has one MI355X, so the model is sharded over ``[cuda:0, cuda:0]`` (two parts on one
+card, device-to-device transport) and over ``[cuda:0]`` with the RCCL transport (a one-GPU communicator:
+the collectives run through RCCL).  The per-element chains are the single-GPU ones, so FedAvg / FedBuff
+are bit-exact against the reference's fixtures; FedYoGi and q-FedAvg keep the single-GPU tolerances
+(see test_gpu_parity.py)."""
+import pickle
+import threading
+import time
+
+import numpy as np
+import pytest
+import torch
+
+from tests.golden_io import Scenario, StateDictModule, assert_state_close, assert_state_equal, scenario_names
+
+pytestmark = pytest.mark.gpu
+
+QFED_RTOL = 1e-5
+YOGI_RTOL = 1e-6
+SHARDINGS = {"two_parts_one_gpu": ([0, 0], "copy"), "rccl_one_gpu": ([0], "rccl")}
+
+
+def _sharded(sc, devices, transport, capacity=None):
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+    from fedscale_amd.cloud.internal.sharded_model_adapter import ShardedModelAdapter
+
+    args = sc.args()
+    model = StateDictModule(sc.names, sc.init_state())
+    opt = TorchServerOptimizer(args.gradient_policy, args, "cuda:0") if sc.meta.get("optimizer") is not None else None
+    return args, opt, ShardedModelAdapter(model, optimizer=opt, devices=devices, staging_capacity=capacity,
+                                          transport=transport)
+
+
+def _yogi_state(adapter):
+    """The sharded YoGi m/v reassembled into the reference's per-tensor lists (yogi.py:11-19)."""
+    L = adapter.layout
+    m = torch.zeros(L.ld)
+    v = torch.zeros(L.ld)
+    for p in adapter.parts:
+        y = p.optimizer.gradient_controller
+        m[p.layout.p0:p.layout.p1] = y.m[:p.layout.P].cpu()
+        v[p.layout.p0:p.layout.p1] = y.v[:p.layout.P].cpu()
+    y0 = adapter.parts[0].optimizer.gradient_controller
+    return L.unpack(m, y0.ms.cpu()), L.unpack(v, y0.vs.cpu())
+
+
+def _check(sc, r, got, adapter, ctx):
+    pol = sc.meta["policy"]
+    if pol == "q-fedavg":
+        assert_state_close(got, sc.expected(r), QFED_RTOL, ctx, int_slack=1)
+    elif pol == "fed-yogi":
+        assert_state_close(got, sc.expected(r), YOGI_RTOL, ctx)
+        m, v = _yogi_state(adapter)
+        (assert_state_equal if r == 0 else lambda g, w, c: assert_state_close(g, w, YOGI_RTOL, c))(m, sc.yogi_state(r)[0], ctx + " m")
+        (assert_state_equal if r == 0 else lambda g, w, c: assert_state_close(g, w, YOGI_RTOL, c))(v, sc.yogi_state(r)[1], ctx + " v")
+    else:
+        assert_state_equal(got, sc.expected(r), ctx)
+
+
+@pytest.mark.parametrize("capacity", [None, 2])
+@pytest.mark.parametrize("sharding", list(SHARDINGS))
+@pytest.mark.parametrize("name", scenario_names())
+def test_sharded_adapter_matches_reference_fixture(gpu_device, name, sharding, capacity):
+    """Every fixture through DeviceAggregator over a ShardedModelAdapter."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator, DeviceAsyncAggregator
+
+    sc = Scenario(name)
+    devices, transport = SHARDINGS[sharding]
+    args, opt, adapter = _sharded(sc, devices, transport, capacity)
+    assert adapter.group.transport == transport
+    if sc.meta["policy"] == "fedbuff":
+        agg = DeviceAsyncAggregator(adapter, args)
+        agg.round = sc.meta["round"]
+        for k, s in enumerate(sc.meta["staleness"]):
+            agg.client_task_model_version[101 + k] = agg.round - s
+    else:
+        agg = DeviceAggregator(adapter, args)
+    for r, ks in sc.rounds():
+        if sc.meta["policy"] == "q-fedavg":
+            args.learning_rate = sc.meta["lrs"][r]
+        agg.start_round(len(ks))
+        for res in sc.results(ks, r):
+            agg.on_result(res)
+        _check(sc, r, adapter.get_weights(), adapter, f"{name} {sharding} r{r} cap={capacity}")
+    adapter.group.close()
+
+
+@pytest.mark.parametrize("name", ["fedavg_wide_k64", "fedyogi_wide_3rounds", "qfedavg_q1_lrdecay"])
+def test_sharded_equals_single_gpu(gpu_device, name):
+    """Two parts vs one GPU on the same inputs: FedAvg and fused FedYoGi bit-identical (same chains), the
+    FedAvg mean (model_weights) bit-identical, q-FedAvg within the fp64 norm re-association."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    sc = Scenario(name)
+    args, _, sharded = _sharded(sc, [0, 0], "copy")
+    opt1 = TorchServerOptimizer(args.gradient_policy, args, "cuda:0") if sc.meta.get("optimizer") is not None else None
+    single = TorchModelAdapter(StateDictModule(sc.names, sc.init_state()), optimizer=opt1, device="cuda:0")
+    aggs = [DeviceAggregator(sharded, args), DeviceAggregator(single, args)]
+    for r, ks in sc.rounds():
+        if sc.meta["policy"] == "q-fedavg":
+            args.learning_rate = sc.meta["lrs"][r]
+        for agg in aggs:
+            agg.start_round(len(ks))
+            for res in sc.results(ks, r):
+                agg.on_result(res)
+        a, b = sharded.get_weights(), single.get_weights()
+        if sc.meta["policy"] == "q-fedavg":
+            assert_state_close(a, [t.numpy() for t in b], 1e-6, f"{name} r{r}", int_slack=1)
+        else:
+            assert_state_equal(a, [t.numpy() for t in b], f"{name} r{r}")
+        assert_state_equal(list(aggs[0].model_weights), list(aggs[1].model_weights), f"{name} mean r{r}")
+
+
+def _executor_payload(res):
+    return pickle.dumps(res)
+
+
+@pytest.mark.parametrize("name", ["fedavg_femnist_cnn_k10", "fedyogi_mixed_3rounds", "qfedavg_q1_lrdecay",
+                                  "fedavg_wide_k64"])
+def test_reference_event_loop_drives_the_sharded_model(gpu_device, name):
+    """The mixin over the reference's event-loop shape (tests/event_loop.py): 4 executor threads upload
+    through CLIENT_EXECUTE_COMPLETION (servicer side, aggregator.py:919-963) and keep pinging
+    (CLIENT_PING, :870-917: create_client_task, get_test_config, UPDATE_MODEL); the main thread reduces
+    in queue order (event_monitor, :965-1007).  The model is sharded 2 ways.  The result equals the oracle
+    run in the realised arrival order; every payload an executor received unpickles to exactly one model
+    version; nothing deadlocks (every wait has a deadline)."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregatorMixin
+    from oracle.cpu_reference import (OracleAggregator, OracleModel, OracleModelAdapter,
+                                      OracleServerOptimizer)
+    from tests import event_loop as EL
+
+    sc = Scenario(name)
+    args, opt, adapter = _sharded(sc, [0, 0], "copy")
+    rounds = [len(ks) for _, ks in sc.rounds()]
+    pol = sc.meta["policy"]
+    if pol == "q-fedavg":
+        args.learning_rate = sc.meta["lrs"][0]
+
+    class A(DeviceAggregatorMixin, EL.Aggregator):
+        pass
+
+    agg = A(adapter, args, rounds)
+    executors = [1, 2, 3, 4]
+    versions = [adapter.get_weights()]  # version 0, then one per round (round_done)
+    payloads = []
+    errors = []
+    stop = threading.Event()
+    results = {k: res for r, ks in sc.rounds() for k, res in zip(ks, sc.results(ks, r))}
+    order = sorted(results)
+    lock = threading.Lock()
+    upload_next = [0]
+
+    def executor(e):
+        try:
+            i = 0
+            while not stop.is_set():
+                with lock:  # executors upload the clients of the CURRENT round only (as in FedScale)
+                    k = None
+                    if upload_next[0] < len(order):
+                        cand = order[upload_next[0]]
+                        r_of = next(r for r, ks in sc.rounds() if cand in ks)
+                        if r_of == agg.round:
+                            k = cand
+                            upload_next[0] += 1
+                if k is not None:
+                    req = EL.request(e, client_id=k, event=EL.UPLOAD_MODEL, data=_executor_payload(results[k]))
+                    ev, meta, data = agg.CLIENT_EXECUTE_COMPLETION(req, None)
+                else:
+                    if i % 3 == 0:
+                        agg.individual_client_events[e].append(EL.CLIENT_TRAIN if i % 2 else EL.MODEL_TEST)
+                    ev, meta, data = agg.CLIENT_PING(EL.request(e, client_id=k or 0), None)
+                if ev in (EL.UPDATE_MODEL, EL.CLIENT_TRAIN, EL.MODEL_TEST):
+                    payloads.append(data)
+                i += 1
+                time.sleep(0.0002)
+        except Exception as ex:  # surfaced by the main thread
+            errors.append(ex)
+
+    def on_round(r):
+        if pol == "q-fedavg" and r + 1 < len(sc.meta["lrs"]):
+            args.learning_rate = sc.meta["lrs"][r + 1]
+
+    threads = [threading.Thread(target=executor, args=(e,), daemon=True) for e in executors]
+    for t in threads:
+        t.start()
+    try:
+        agg.event_monitor(executors, deadline_s=60, on_round=on_round)
+        for e in executors:
+            agg.individual_client_events[e].append(EL.UPDATE_MODEL)
+        time.sleep(0.05)
+    finally:
+        stop.set()
+        for t in threads:
+            t.join(timeout=30)
+    assert not any(t.is_alive() for t in threads), "an executor thread is stuck"
+    assert not errors, errors
+    versions += agg.round_done
+
+    # the oracle, fed in the order the main loop reduced
+    oargs = sc.args()
+    if pol == "q-fedavg":
+        oargs.learning_rate = sc.meta["lrs"][0]
+    oracle = OracleAggregator(OracleModelAdapter(OracleModel(sc.names, sc.init_state()),
+                                                 OracleServerOptimizer(oargs.gradient_policy, oargs)), oargs)
+    idx = {res["client_id"]: k for k, res in results.items()}
+    done = 0
+    for r, K in enumerate(rounds):
+        if pol == "q-fedavg":
+            oargs.learning_rate = sc.meta["lrs"][r]
+        oracle.start_round(K)
+        for cid in agg.processed[done:done + K]:
+            oracle.on_result(results[idx[cid]])
+        done += K
+        want = oracle.model_wrapper.get_weights()
+        got = versions[r + 1]
+        if pol == "q-fedavg":
+            assert_state_close(got, [t.numpy() for t in want], QFED_RTOL, f"{name} r{r}", int_slack=1)
+        elif pol == "fed-yogi":
+            assert_state_close(got, [t.numpy() for t in want], YOGI_RTOL, f"{name} r{r}")
+            oracle.model_wrapper.model.load_state_dict(dict(zip(sc.names, got)))  # same trajectory
+        else:
+            assert_state_equal(got, [t.numpy() for t in want], f"{name} r{r}")
+
+    # every egress payload is exactly one model version
+    assert payloads, "no egress happened while the rounds ran"
+    for data in payloads:
+        w = pickle.loads(data)
+        assert isinstance(w, list)
+        assert any(all(torch.equal(a, b) for a, b in zip(w, v)) for v in versions), "a payload mixes versions"
+    adapter.group.close()
+
+
+def test_egress_is_consistent_under_concurrent_rounds(gpu_device):
+    """8 threads call create_client_task / get_test_config / serialize_response of
+    get_weights() (the servicer's paths, aggregator.py:788-816, 902-909) while the main thread completes
+    20 rounds; every payload must unpickle to exactly one committed model version (single GPU and sharded)."""
+    from fedscale_amd import synth
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.sharded_model_adapter import ShardedModelAdapter
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+    from tests import event_loop as EL
+
+    names, shapes = ["w", "b", "n"], [(1024, 1031), (77,), ()]
+    dtypes = [torch.float32, torch.float32, torch.int64]
+    for make in (lambda m: TorchModelAdapter(m, device="cuda:0"),
+                 lambda m: ShardedModelAdapter(m, devices=[0, 0], transport="copy")):
+        adapter = make(synth.LayoutModule(names, shapes, dtypes))
+
+        class A(DeviceAggregator):
+            resource_manager = EL._Resources()
+
+            def get_client_conf(self, cid):
+                return {}
+
+        agg = A(adapter)
+        rng = np.random.default_rng(0)
+        versions = {0: adapter.get_weights()}
+        payloads = []
+        stop = threading.Event()
+        errors = []
+
+        def servicer(i):
+            try:
+                while not stop.is_set():
+                    j = len(payloads) % 3
+                    if j == 0:
+                        _, w = agg.create_client_task(i)
+                    elif j == 1:
+                        _, w = agg.get_test_config(i)
+                    else:
+                        w = adapter.get_weights()
+                    payloads.append(agg.serialize_response(w))
+            except Exception as ex:
+                errors.append(ex)
+
+        threads = [threading.Thread(target=servicer, args=(i,), daemon=True) for i in range(8)]
+        for t in threads:
+            t.start()
+        try:
+            for r in range(20):
+                agg.start_round(3)
+                for k in range(3):
+                    up = {"w": rng.standard_normal(shapes[0], dtype=np.float32),
+                          "b": rng.standard_normal(shapes[1], dtype=np.float32), "n": np.array(r * 3 + k)}
+                    agg.on_result({"client_id": k, "update_weight": up, "moving_loss": 1.0})
+                versions[r + 1] = adapter.get_weights()
+        finally:
+            stop.set()
+            for t in threads:
+                t.join(timeout=30)
+        assert not any(t.is_alive() for t in threads) and not errors, errors
+        assert len(payloads) > 20
+        for data in payloads:
+            w = pickle.loads(data)
+            assert sum(all(torch.equal(a, b) for a, b in zip(w, v)) for v in versions.values()) >= 1
+        if hasattr(adapter, "group"):
+            adapter.group.close()
+
+
+def test_rccl_collectives_one_gpu(gpu_device):
+    """fa_rccl_* with a one-GPU communicator: all-gather, all-reduce, gather and broadcast run through
+    RCCL (ncclCommInitAll + grouped calls) and give the identities a world of one implies; the fixed-order
+    f64 row sum combines per-shard partials."""
+    from fedscale_amd import kernels as kx
+    from fedscale_amd.state import DeviceGroup
+
+    g = DeviceGroup([0], transport="rccl")
+    x = torch.randn(1000, dtype=torch.float64, device="cuda:0")
+    out = torch.empty(1000, dtype=torch.float64, device="cuda:0")
+    g.all_gather([x], [out])
+    assert torch.equal(out, x)
+    y = torch.randn(333, device="cuda:0")
+    root = torch.empty(333, device="cuda:0")
+    g.gather([y], root)
+    assert torch.equal(root, y)
+    b = [y.clone()]
+    g.broadcast(b)
+    assert torch.equal(b[0], y)
+    s = x.clone()
+    g.sum_f64([s])
+    assert torch.equal(s, x)
+    rows = torch.randn(5, 77, dtype=torch.float64, device="cuda:0")
+    o = torch.empty(77, dtype=torch.float64, device="cuda:0")
+    kx.sum_rows_f64(rows, o)
+    want = rows[0].clone()
+    for i in range(1, 5):
+        want = want + rows[i]
+    assert torch.equal(o, want)
+    g.close()
+
+
+def test_nccl_process_group_collectives_world1(gpu_device):
+    """The torch.distributed (RCCL) branch of ShardGroup with device tensors, at world size 1 on the box:
+    all_gather_into_tensor and all_reduce run through the nccl backend (the N-GPU SPMD bench uses them)."""
+    import os
+
+    import torch.distributed as dist
+
+    from fedscale_amd.state import ShardGroup
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29533")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda:0"))
+    try:
+        g = ShardGroup(0, 1)
+        x = torch.arange(4096, dtype=torch.float32, device="cuda:0")
+        assert torch.equal(g.collective_all_gather(x), x)
+        s = torch.ones(100, dtype=torch.float64, device="cuda:0")
+        g.collective_all_reduce(s)
+        assert torch.equal(s, torch.ones_like(s))
+        assert dist.get_backend() == "nccl"
+    finally:
+        dist.destroy_process_group()

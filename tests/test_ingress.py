@@ -280,7 +280,7 @@ def test_client_ping_update_model_hands_out_the_egress_handle():
         def egress_handle(self):
             return "HANDLE"
 
-        def _host_copy(self):
+        def _acquire_host(self):
             self.clones += 1
             raise LookupError("clone path")
 
