@@ -1,23 +1,35 @@
-"""Benchmark: device-resident FedAvg reduction of K x P fp32 client updates on MI355X.
+"""Benchmark: device-resident reduction of K x P fp32 client updates on MI355X (FedScale's aggregator hot
+path, aggregator.py:489-511 + the server step, optimizers.py:31-108).
 
-Workload (BASELINE.json north_star target): K = 1000 clients x P = 25,000,000 fp32 parameters per GPU,
-FedAvg (aggregator.py:489-511): out = (sum of the K updates in arrival order) / K, one fused HIP kernel
-(fa_reduce, FA_FINALIZE).  Inputs are generated on the device before the timed region and stay in HBM.
+Headline workload (BASELINE.json north_star target): FedAvg, K = 1000 clients x P = 25,000,000 fp32
+parameters, one fused HIP kernel (fa_reduce, FA_FINALIZE): out = (sum of the K updates in arrival order)/K.
+Inputs are generated on the device before the timed region and stay in HBM.
 
-A "step" is one aggregation round over the resident K x P batch.  With --gpus N (one process per GPU,
-torchrun) every rank owns an equal 25M-parameter shard of an N x 25M-parameter model and reduces its
-K client slices: weak scaling, no data-path collective.  ``value`` counts client updates of one 25M-fp32
-(100 MB) slice across all ranks per second.  ``--shard clients`` is the other layout of SURVEY §8e: every
-rank reduces its own K clients of a whole 25M-parameter model, then one RCCL all-reduce of the partial
-sums (inside the timed step) and the replicated finish; ``value`` = N*K client updates per second.  --reassemble additionally times the RCCL all-gather that
-rebuilds the global model for egress (reported as ``reassembly_ms``, not part of ``value``).
+A "step" is one aggregation round over the resident K x P batch.
+
+--gpus N (one process per GPU, torchrun; RCCL over xGMI) shards THE SAME model over the ranks (strong
+scaling, the north star's "1000 x 25M ... >= 3.5x at 8 GPUs"): rank r owns the 64-aligned parameter slice
+[r*S, (r+1)*S), S = ceil(P/N) rounded up to 64, and reduces its slice of every client update — no
+data-path collective (each output element depends only on its own column).  ``value`` = K * steps / wall
+(max over ranks): client updates of the whole model per second.  The RCCL all-gather that reassembles the
+global model for egress is timed separately (``reassembly_ms``), outside ``value``.
+``--scaling weak`` keeps round 1's alternative (every rank a 25M shard of an N x 25M model, value = N*K*steps
+/ wall); ``--shard clients`` is SURVEY §8e's other layout (every rank reduces K clients of the whole model,
+then one RCCL all-reduce of the partial chains inside the step; value = N*K*steps/wall).
+
+--config c2 | c3 | c4 | c5 runs a BASELINE config as the headline line instead (c4 = 1000 x 25M FedYoGi,
+c5 = 10000 x 100M q-FedAvg streamed through a resident chunk of <= 1000 clients); at N>1 they are sharded
+the same way.  The default run also reports configs 4 and 5 sharded over the N ranks under
+``other_configs`` (so the driver's 4- and 8-GPU runs measure them at their BASELINE GPU counts), and at
+N=1 configs 1-3 plus each config's CPU leg.
 
 Extra objects on the JSON line:
-  roofline     achieved algorithmic GB/s of the reduce kernel (4KP+4P bytes per launch / mean launch time
-               from HIP events on the launch stream) vs the 8 TB/s HBM3E peak; ``traffic`` = HBM bytes
-               per launch from the rocprofv3 PMC summary committed under profiles/ (null if absent)
-  cpu_baseline the CPU oracle (numpy restatement of aggregator.py:497-507, bit-exact to the reference's
-               golden vectors) timed on this host on a bounded sample of the same workload (rank 0, N=1)
+  roofline     achieved algorithmic GB/s of the dominant kernel on one GPU (algorithmic bytes per launch,
+               SURVEY §8d, over this rank's slice / mean launch time from HIP events on the launch stream)
+               vs the 8 TB/s HBM3E peak; ``traffic`` = HBM bytes per launch from the rocprofv3 PMC summary
+               committed under profiles/ (null if absent)
+  cpu_baseline the CPU oracle (restatement of aggregator.py:497-507, bit-exact to the reference's golden
+               vectors) timed on this host on a bounded sample of the same workload (rank 0, N=1)
 """
 from __future__ import annotations
 
@@ -34,60 +46,163 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 PMC_FILE = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
+# BASELINE.json configs as device workloads (config 1 is the host round, measured separately)
+CONFIGS = {
+    "headline": dict(policy="fedavg", clients=1000, params=25_000_000),
+    "c2": dict(policy="fedavg", clients=100, params=1_000_000),
+    "c3": dict(policy="fedavg", clients=1000, params=11_191_242),
+    "c4": dict(policy="fedyogi", clients=1000, params=25_000_000),
+    "c5": dict(policy="qfedavg", clients=10_000, params=100_000_000),
+}
+EXTRA_BYTES = {  # SURVEY §8d algorithmic bytes beyond the 4KP client read + 4P model write, per GPU slice
+    "fedavg": lambda K, P: 0, "fedbuff": lambda K, P: 4 * K, "fedyogi": lambda K, P: 20 * P,
+    "qfedavg": lambda K, P: 4 * P + 8 * K}
+
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--clients", type=int, default=1000)
-    ap.add_argument("--params", type=int, default=25_000_000, help="fp32 parameters per GPU shard")
-    ap.add_argument("--policy", default="fedavg", choices=["fedavg", "fedyogi", "fedbuff", "qfedavg"])
+    ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
+    ap.add_argument("--clients", type=int, default=None, help="override the config's K")
+    ap.add_argument("--params", type=int, default=None,
+                    help="override the config's P (the whole model; per GPU with --scaling weak)")
+    ap.add_argument("--policy", default=None, choices=["fedavg", "fedyogi", "fedbuff", "qfedavg"])
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"])
     ap.add_argument("--shard", default="params", choices=["params", "clients"],
                     help="params: each rank reduces its slice of the model for every client (no data-path "
                          "collective, bit-exact); clients: each rank reduces its own K clients over the whole "
                          "model, then one RCCL all-reduce of the partial sums (state.py)")
-    ap.add_argument("--reassemble", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline sample (0 = skip)")
+    ap.add_argument("--no-reassemble", action="store_true", help="skip the egress all-gather timing at N>1")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the headline CPU sample (0 = skip "
+                                                                     "every CPU leg)")
     ap.add_argument("--seed", type=int, default=2024)
-    ap.add_argument("--no-other-configs", action="store_true",
-                    help="skip the BASELINE configs 2/3 side measurements (reported under other_configs)")
+    ap.add_argument("--no-other-configs", action="store_true", help="skip the side measurements (other_configs)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse ranks sharing a GPU")
-    return ap.parse_args()
+    a = ap.parse_args()
+    cfg = dict(CONFIGS[a.config])
+    for k in ("clients", "params", "policy"):
+        if getattr(a, k) is not None:
+            cfg[k] = getattr(a, k)
+    a.cfg = cfg
+    return a
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU baseline legs (the oracle on this host: bench.py is the one product-side file allowed to call it)
+# ------------------------------------------------------------------------------------------------
+def _host_info() -> dict:
+    import torch
+
+    model = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"host_cpu": model, "host_cpus": os.cpu_count(), "torch_threads": torch.get_num_threads()}
+
+
+def _pool(P: int, n: int, seed: int):
+    """n distinct fp32 client buffers of P elements (> LLC each for the large configs): one normal draw,
+    then cheap distinct scalings (values only need to be ordinary floats for the timing)."""
+    import numpy as np
+
+    rng = np.random.default_rng(seed)
+    base = rng.standard_normal(P, dtype=np.float32) * np.float32(0.05)
+    return [base * np.float32(1.0 + 1e-3 * i) for i in range(n)]
+
+
+def _cpu_accumulate(pool, K: int, budget_s: float):
+    """Per-client accumulate cost of aggregator.py:497-503 (numpy add, a new array per client) on a
+    rotating pool; returns (s per client, clients timed, last accumulator)."""
+    from oracle.cpu_reference import fedavg_step
+
+    acc = fedavg_step(None, [pool[0]], True)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        acc = fedavg_step(acc, [pool[(n + 1) % len(pool)]], False)
+        n += 1
+        if time.perf_counter() - t0 > budget_s or n >= K - 1:
+            break
+    return (time.perf_counter() - t0) / n, n + 1, acc
+
+
+def cpu_leg(policy: str, K: int, P: int, budget_s: float, seed: int, pool_n: int = 16) -> dict:
+    """The oracle's round for one config on this host: accumulate (per client, extrapolated to K) and
+    finalize timed separately; q-FedAvg's finalize loop over the K retained results is
+    timed on a subsample at two sizes (per-client slope + fixed part) and extrapolated."""
+    import argparse as _ap
+    import copy
+
+    import numpy as np
+    import torch
+
+    from oracle.cpu_reference import (OracleModel, OracleModelAdapter, OracleServerOptimizer, fedavg_close)
+
+    pool = _pool(P, pool_n, seed)
+    t_acc, n_acc, acc = _cpu_accumulate(pool, K, budget_s * (0.5 if policy != "fedavg" else 0.9))
+    out = {"policy": policy, "clients": K, "params": P, "accumulate_ms_per_client": t_acc * 1e3,
+           "accumulate_clients_timed": n_acc, "pool_buffers": pool_n, "kind": "port"}
+    t1 = time.perf_counter()
+    mean = fedavg_close(acc, K)
+    t_div = time.perf_counter() - t1
+    args = _ap.Namespace(gradient_policy=None, yogi_eta=3e-3, yogi_tau=1e-8, yogi_beta=0.9, yogi_beta2=0.99,
+                         learning_rate=0.05, qfed_q=1.0)
+    if policy == "fedavg":
+        t_fin = t_div
+    elif policy == "fedyogi":
+        args.gradient_policy = "fed-yogi"
+        ad = OracleModelAdapter(OracleModel(["w"], [torch.from_numpy(pool[1].copy())]),
+                                OracleServerOptimizer("fed-yogi", args))
+        ad.set_weights(copy.deepcopy(mean))  # lazy YoGi state init (yogi.py:17-19) outside the timing
+        t1 = time.perf_counter()
+        ad.set_weights(copy.deepcopy(mean))  # torch_model_adapter.py:23-39 -> optimizers.py:43-63
+        t_fin = t_div + time.perf_counter() - t1
+    else:
+        args.gradient_policy = "q-fedavg"
+        rng = np.random.default_rng(seed)
+        ts = []
+        for n in (2, 4):
+            res = [{"update_weight": [pool[(i + 2) % pool_n]], "moving_loss": float(rng.uniform(0.5, 2.0))}
+                   for i in range(n)]
+            ad = OracleModelAdapter(OracleModel(["w"], [torch.from_numpy(pool[1].copy())]),
+                                    OracleServerOptimizer("q-fedavg", args))
+            t1 = time.perf_counter()
+            ad.set_weights(copy.deepcopy(mean), client_training_results=res)  # optimizers.py:65-104
+            ts.append(time.perf_counter() - t1)
+        per = max(1e-9, (ts[1] - ts[0]) / 2)
+        fixed = max(0.0, ts[0] - 2 * per)
+        out["finalize_ms_per_retained_client"] = per * 1e3
+        t_fin = t_div + fixed + per * K
+    t_round = t_acc * (K - 1) + t_fin
+    out.update({"finalize_ms": t_fin * 1e3, "round_s": t_round, "client_updates_per_s": K / t_round,
+                "hbm_equiv_gbps": (4 * K * P + 4 * P + EXTRA_BYTES[policy](K, P)) / t_round / 1e9,
+                "cores": 1 if policy == "fedavg" else torch.get_num_threads(),
+                "sample": f"{n_acc} of {K} client adds timed on a {pool_n}-buffer pool, extrapolated linearly"})
+    del pool
+    return out
 
 
 def cpu_baseline(K: int, P: int, budget_s: float, seed: int) -> dict:
-    """Time the oracle's FedAvg restatement on host cores on a K-subsample, extrapolated to K."""
-    import numpy as np
-
-    from oracle.cpu_reference import fedavg_close, fedavg_step
-
-    rng = np.random.default_rng(seed)
-    pool_n = 8
-    base = rng.standard_normal(P, dtype=np.float32) * np.float32(0.05)
-    pool = [base + rng.standard_normal(P, dtype=np.float32) * np.float32(0.01) for _ in range(pool_n)]
-    # per-client accumulate cost (aggregator.py:500-503: one numpy add per tensor, new array each time)
-    acc = fedavg_step(None, [pool[0]], True)
-    n = 0
-    t0 = time.perf_counter()
-    while True:
-        acc = fedavg_step(acc, [pool[(n + 1) % pool_n]], False)
-        n += 1
-        if time.perf_counter() - t0 > budget_s * 0.8 or n >= K - 1:
-            break
-    t_acc = (time.perf_counter() - t0) / n
-    t1 = time.perf_counter()
-    fedavg_close(acc, K)
-    t_fin = time.perf_counter() - t1
-    t_round = t_acc * (K - 1) + t_fin
-    return {"value": K / t_round, "unit": "client-updates/s", "cores": 1, "kind": "port",
-            "sample": f"oracle FedAvg (numpy, single-threaded) over {n + 1} of the {K} x {P} fp32 client updates "
-                      f"(pool of {pool_n} distinct 100 MB buffers), {t_acc * 1e3:.1f} ms/client + "
-                      f"{t_fin * 1e3:.0f} ms finalize, extrapolated linearly to K={K}",
-            "host": platform.processor() or platform.machine(), "host_cpus": os.cpu_count()}
+    """The headline's CPU leg: the oracle's FedAvg on a K-subsample, extrapolated to K."""
+    leg = cpu_leg("fedavg", K, P, budget_s, seed)
+    return dict({"value": leg["client_updates_per_s"], "unit": "client-updates/s", "cores": 1, "kind": "port",
+                 "sample": (f"oracle FedAvg (numpy, single-threaded) over {leg['accumulate_clients_timed']} of the "
+                            f"{K} x {P} fp32 client updates (pool of {leg['pool_buffers']} distinct "
+                            f"{4 * P / 1e6:.0f} MB buffers), {leg['accumulate_ms_per_client']:.1f} ms/client + "
+                            f"{leg['finalize_ms']:.0f} ms finalize, extrapolated linearly to K={K}")},
+                **_host_info())
 
 
+# ------------------------------------------------------------------------------------------------
+# config 1: the whole host round through the drop-in
+# ------------------------------------------------------------------------------------------------
 def _c1_updates(seed: int, K: int):
     """Config 1's inputs: K FEMNIST small-CNN updates (P = 24,492) as the executor's result dicts hold
     them (torch_client.py:76-91: numpy arrays in host memory)."""
@@ -153,141 +268,227 @@ def cpu_baseline_c1(seed: int, rounds: int = 50) -> dict:
     return {"round_ms": ms, "client_updates_per_s": K / (ms * 1e-3), "cores": 1, "kind": "port"}
 
 
-def other_configs(dev, seed: int) -> dict:
-    """BASELINE.json configs 2 and 3 on one GPU (FedAvg, device-resident), beside the headline line, plus
-    one GPU's shard of configs 4 and 5 (``shard_configs``).
-    Config 2 (400 MB) rotates two input sets so the 256 MiB Infinity Cache cannot serve repeats."""
+# ------------------------------------------------------------------------------------------------
+# device workloads
+# ------------------------------------------------------------------------------------------------
+class Workload:
+    """One aggregation round of ``policy`` over K clients of a P-parameter model, on this rank's slice
+    (parameter sharding over ``world`` ranks; the whole model when world == 1 or client mode).
+
+    The client updates are resident in HBM: C <= K rows; a round with K > C streams K/C passes over the
+    resident chunk (each pass reads its full 4*C*P bytes from HBM — the refill that ingress would do is
+    not part of the device throughput), continuing one chain / delta across the passes exactly as the
+    device path's chunk folding does."""
+
+    def __init__(self, policy, K, P_total, rank, world, dev, seed, shards, *, weak=False, chunk=None,
+                 budget_fraction=0.6, sets=1):
+        import numpy as np
+        import torch
+
+        from fedscale_amd import kernels as kx
+        from fedscale_amd import synth
+        from fedscale_amd.bucket import round_up
+
+        self.policy, self.K, self.world, self.dev, self.shards = policy, K, world, dev, shards
+        self.cmode = shards.shards_clients
+        if weak or self.cmode or world == 1:
+            self.P, self.P_total = P_total, P_total * (world if weak else 1)
+            ld = round_up(P_total, 64)
+        else:
+            S = round_up(max(1, -(-P_total // world)), 64)
+            p0 = min(P_total, rank * S)
+            self.P, self.P_total = min(P_total, p0 + S) - p0, P_total
+            ld = S
+        self.ld = ld
+        free, _ = torch.cuda.mem_get_info(dev)
+        cap = max(1, int(free * budget_fraction) // (4 * ld * sets))
+        if policy == "qfedavg":
+            cap = min(cap, kx.qfed_max_chunk())
+        self.C = min(K, cap, chunk or K)
+        self.passes = [(k0, min(self.C, K - k0)) for k0 in range(0, K, self.C)]
+        self.xs = []
+        for i in range(sets):  # sets > 1: rotate input sets so the 256 MiB Infinity Cache cannot serve repeats
+            x = torch.empty(self.C, ld, dtype=torch.float32, device=dev)
+            synth.fill(x, self.C, self.P, seed=seed + 7919 * rank + 31 * i)
+            self.xs.append(x)
+        self.it = 0
+        self.out = torch.zeros(ld, dtype=torch.float32, device=dev)
+        self.acc = torch.zeros(ld, dtype=torch.float32, device=dev) if (self.cmode or len(self.passes) > 1) else None
+        self.Kg = K * world if self.cmode else K  # clients in the round (client mode: every rank brings K)
+        self.denom = float(np.float32(self.Kg))
+        self.a = None
+        if policy == "fedbuff":
+            s = [1 / (1 + (k % 6)) ** 0.5 for k in range(self.Kg)]
+            self.a = torch.tensor(np.asarray(s[rank * K:(rank + 1) * K] if self.cmode else s, dtype=np.float32),
+                                  device=dev)
+            self.denom = float(np.float32(sum(s)))
+        self.yogi = None
+        if policy == "fedyogi":
+            self.yogi = dict(last=torch.zeros(ld, device=dev), m=torch.zeros(ld, device=dev),
+                             v=torch.zeros(ld, device=dev), eta=float(np.float32(3e-3)), tau=float(np.float32(1e-8)),
+                             beta=float(np.float32(0.9)), omb=float(np.float32(1 - 0.9)),
+                             omb2=float(np.float32(1 - 0.99)), init=False)
+            synth.fill(self.yogi["last"].view(1, -1), 1, self.P, seed=seed + 1)
+        self.qf = None
+        if policy == "qfedavg":
+            rng = np.random.default_rng(seed)
+            losses = rng.uniform(0.5, 2.0, size=self.Kg)
+            lr, q = 0.05, 1.0
+            mine = losses[rank * K:(rank + 1) * K] if self.cmode else losses
+            self.qf = dict(last=torch.empty(1, ld, device=dev), delta=torch.zeros(ld, device=dev),
+                           sq=torch.zeros(self.Kg, dtype=torch.float64, device=dev),
+                           ws=kx.qfed_workspace(self.C, dev), hs=torch.zeros(2, device=dev), lr=lr,
+                           alpha=torch.tensor([np.float32(np.float_power(l + 1e-10, q)) for l in mine], device=dev),
+                           c1=torch.tensor([np.float32(q * np.float_power(l + 1e-10, q - 1)) for l in losses],
+                                           device=dev),
+                           c2=torch.tensor([np.float32((1 / lr) * np.float_power(l + 1e-10, q)) for l in losses],
+                                           device=dev))
+            synth.fill(self.qf["last"], 1, self.P, seed=seed + (0 if self.cmode else 7919 * rank), scale_noise=0.0)
+            self.qf["last"] = self.qf["last"][0]
+        self.stream = torch.cuda.current_stream(dev)
+
+    @property
+    def alg_bytes(self) -> int:
+        """SURVEY §8d algorithmic bytes of this rank's dominant kernel(s) per round."""
+        return 4 * self.K * self.P + 4 * self.P + EXTRA_BYTES[self.policy](self.K, self.P)
+
+    def step(self, ev=None):
+        from fedscale_amd import kernels as kx
+
+        x = self.xs[self.it % len(self.xs)]
+        self.it += 1
+        K, P, st = self.K, self.P, self.stream
+        if ev is not None:
+            ev[0].record(st)
+        if self.qf is not None:  # optimizers.py:73-104: phase 1 (timed as the dominant kernel), hs, phase 2
+            qf = self.qf
+            qf["sq"].zero_()
+            kb = self.shards.rank * K if self.cmode else 0
+            for i, (k0, n) in enumerate(self.passes):
+                kx.qfed_accumulate(x, n, P, last=qf["last"], alpha=qf["alpha"][k0:k0 + n], lr=qf["lr"],
+                                   delta=qf["delta"], sqnorm=qf["sq"][kb + k0:kb + k0 + n], workspace=qf["ws"],
+                                   accumulate=i > 0)
+            if ev is not None:
+                ev[1].record(st)
+            if self.cmode:  # per-rank partial delta chains + each client's norm from its owner rank
+                self.shards.all_reduce_sum(qf["delta"])
+                self.shards.all_reduce_sum(qf["sq"])
+            elif self.world > 1:  # the one exchange of parameter sharding: per-client norms over the shards
+                self.shards.all_reduce_sum(qf["sq"])
+            kx.qfed_hs(qf["sq"], qf["c1"], qf["c2"], self.Kg, qf["hs"])
+            kx.qfed_finalize(qf["last"], qf["delta"], qf["hs"], self.out, P)
+            return
+        last = len(self.passes) - 1
+        for i, (k0, n) in enumerate(self.passes):
+            a = self.a[k0:k0 + n] if self.a is not None else None
+            acc_in = self.acc if i > 0 else None
+            if i < last or self.cmode:  # chain only: a middle pass, or this rank's partial (client mode)
+                kx.reduce(x, n, P, self.acc, a=a, acc_in=acc_in)
+            elif self.yogi is None:
+                kx.reduce(x, n, P, self.out, a=a, acc_in=acc_in, denom=self.denom, finalize=True)
+            else:
+                kx.reduce_yogi(x, n, P, out=self.out, a=a, acc_in=acc_in, denom=self.denom, **self.yogi)
+        if ev is not None:
+            ev[1].record(st)
+        if self.cmode:  # partial chain of this rank's clients, RCCL all-reduce, finish on the summed vector
+            self.shards.all_reduce_sum(self.acc)
+            x1 = self.acc.view(1, self.ld)
+            if self.yogi is None:
+                kx.reduce(x1, 1, P, self.out, denom=self.denom, finalize=True)
+            else:
+                kx.reduce_yogi(x1, 1, P, out=self.out, denom=self.denom, **self.yogi)
+
+    def free(self):
+        import torch
+
+        self.xs = []
+        self.acc = self.out = self.qf = self.yogi = None
+        torch.cuda.empty_cache()
+
+
+def _sync_all(dev, world):
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+
+
+def _max_over_ranks(vals, dev, world, backend):
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor(vals, dtype=torch.float64)
+    if world > 1:
+        if backend == "nccl":
+            t = t.to(dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.cpu()]
+
+
+def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend):
+    """Warmup, then exactly ``steps`` rounds between barrier + synchronize; (wall s, mean dominant-kernel
+    ms), both max over ranks."""
     import numpy as np
     import torch
 
-    from fedscale_amd import kernels as kx
-    from fedscale_amd import synth
-    from fedscale_amd.bucket import round_up
+    for _ in range(warmup):
+        w.step()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    _sync_all(dev, world)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        w.step(evs[i])
+    _sync_all(dev, world)
+    wall = time.perf_counter() - t0
+    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    return _max_over_ranks([wall, kern_ms], dev, world, backend), kern_ms
 
-    out = {"c1_femnist_cnn_k10_host_round": c1_host_round(dev, seed)}
-    for name, K, P, sets in (("c2_synthetic_k100_p1M", 100, 1_000_000, 2),
-                             ("c3_resnet18_layout_k1000_p11191242", 1000, 11_191_242, 1)):
-        ld = round_up(P, 64)
-        xs = []
-        for i in range(sets):
-            x = torch.empty(K, ld, dtype=torch.float32, device=dev)
-            synth.fill(x, K, P, seed=seed + 31 * i)
-            xs.append(x)
-        o = torch.empty(ld, dtype=torch.float32, device=dev)
-        for i in range(4):
-            kx.reduce(xs[i % sets], K, P, o, denom=float(np.float32(K)), finalize=True)
-        torch.cuda.synchronize(dev)
-        evs = []
-        for i in range(20):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            kx.reduce(xs[i % sets], K, P, o, denom=float(np.float32(K)), finalize=True)
-            e1.record()
-            evs.append((e0, e1))
-        torch.cuda.synchronize(dev)
-        ms = float(np.median([a.elapsed_time(b) for a, b in evs]))
-        out[name] = {"clients": K, "params": P, "kernel_ms": ms, "client_updates_per_s": K / (ms * 1e-3),
-                     "hbm_gbps": (4 * K * P + 4 * P) / (ms * 1e-3) / 1e9}
-        del xs, o
-        torch.cuda.empty_cache()
-    out.update(shard_configs(dev, seed))
+
+def config_line(name, cfg, dev, rank, world, shards, seed, backend, steps=5, warmup=2, **kw) -> dict:
+    """A BASELINE config on all ranks (parameter-sharded over them), for other_configs."""
+    w = Workload(cfg["policy"], cfg["clients"], cfg["params"], rank, world, dev, seed, shards, **kw)
+    (wall, kern_max), _ = time_workload(w, steps, warmup, dev, world, backend)
+    ms = wall * 1e3 / steps
+    out = {"policy": cfg["policy"], "clients": cfg["clients"], "params": cfg["params"], "n_gpus": world,
+           "params_per_gpu": w.P, "resident_clients": w.C, "passes": len(w.passes), "round_ms": ms,
+           "client_updates_per_s": cfg["clients"] / (ms * 1e-3),
+           "hbm_gbps_per_gpu": w.alg_bytes / (ms * 1e-3) / 1e9, "dominant_kernel_ms": kern_max,
+           "hbm_gbps_kernel": w.alg_bytes / (kern_max * 1e-3) / 1e9}
+    if len(w.passes) > 1:
+        out["note"] = ("K > resident chunk: each round streams %d passes over the resident %d clients (every pass "
+                       "reads its 4*C*P bytes from HBM; the ingress refill is not part of this device rate)"
+                       % (len(w.passes), w.C))
+    w.free()
     return out
 
 
-def _timed(fn, reps, stream):
-    import numpy as np
-    import torch
-
-    evs = []
-    for _ in range(reps):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record(stream)
-        fn()
-        e1.record(stream)
-        evs.append((e0, e1))
-    torch.cuda.synchronize()
-    return [a.elapsed_time(b) for a, b in evs]
-
-
-def shard_configs(dev, seed: int) -> dict:
-    """One GPU's share of the multi-GPU BASELINE configs (the 4- and 8-GPU runs are the driver's):
-    config 4 = 1000 clients x 25M params FedYoGi over 4 GPUs -> a 6.25M-parameter shard per GPU, fused
-    reduce + FedYoGi (fa_reduce_yogi, 4KP + 24P bytes); config 5 = 10000 clients x 100M params q-FedAvg over
-    8 GPUs -> a 12.5M-parameter shard per GPU, the 10000 clients streamed through one 1000-client staging
-    buffer (50 GB) as the device path does: 10 fa_qfed_accumulate launches continuing one delta chain,
-    then hs + the step.  Refilling the staging buffer (on-device generator, standing in for the H2D
-    ingress) is outside the timed launches; the timed region is every kernel of the round."""
-    import numpy as np
-    import torch
-
-    from fedscale_amd import kernels as kx
-    from fedscale_amd import synth
-    from fedscale_amd.bucket import round_up
-
-    stream = torch.cuda.current_stream(dev)
-    out = {}
-    # ---- config 4 shard: FedYoGi ------------------------------------------------------------------
-    K, P = 1000, 25_000_000 // 4
-    ld = round_up(P, 64)
-    x = torch.empty(K, ld, dtype=torch.float32, device=dev)
-    synth.fill(x, K, P, seed=seed + 4)
-    st = {n: torch.zeros(ld, device=dev) for n in ("last", "m", "v", "out")}
-    synth.fill(st["last"].view(1, -1), 1, P, seed=seed + 5, scale_noise=0.0)
-    hp = dict(eta=float(np.float32(3e-3)), tau=float(np.float32(1e-8)), beta=float(np.float32(0.9)),
-              omb=float(np.float32(1 - 0.9)), omb2=float(np.float32(1 - 0.99)))
-
-    def yogi_round(init=False):
-        kx.reduce_yogi(x, K, P, last=st["last"], m=st["m"], v=st["v"], out=st["out"], denom=float(np.float32(K)),
-                       init=init, **hp)
-
-    yogi_round(True)
-    ms = float(np.median(_timed(yogi_round, 10, stream)))
-    out["c4_fedyogi_shard_k1000_p6250000"] = {
-        "clients": K, "params_per_gpu": P, "of": "1000 x 25M FedYoGi over 4 GPUs", "round_ms": ms,
-        "client_updates_per_s": K / (ms * 1e-3), "hbm_gbps": (4 * K * P + 24 * P) / (ms * 1e-3) / 1e9}
-    del x, st
-    torch.cuda.empty_cache()
-    # ---- config 5 shard: q-FedAvg, streamed -------------------------------------------------------
-    Ktot, C, P = 10_000, min(1000, kx.qfed_max_chunk()), 100_000_000 // 8
-    ld = round_up(P, 64)
-    x = torch.empty(C, ld, dtype=torch.float32, device=dev)
-    last = torch.empty(1, ld, dtype=torch.float32, device=dev)
-    synth.fill(last, 1, P, seed=seed + 6, scale_noise=0.0)
-    last = last[0]
-    rng = np.random.default_rng(seed)
-    losses = rng.uniform(0.5, 2.0, size=Ktot)
-    lr, q = 0.05, 1.0
-    alpha = torch.tensor([np.float32(np.float_power(l + 1e-10, q)) for l in losses], device=dev)
-    c1 = torch.tensor([np.float32(q * np.float_power(l + 1e-10, q - 1)) for l in losses], device=dev)
-    c2 = torch.tensor([np.float32((1 / lr) * np.float_power(l + 1e-10, q)) for l in losses], device=dev)
-    delta = torch.zeros(ld, device=dev)
-    sq = torch.zeros(Ktot, dtype=torch.float64, device=dev)
-    ws = kx.qfed_workspace(C, dev)
-    hs = torch.zeros(2, device=dev)
-    new = torch.zeros(ld, device=dev)
-    kern = []
-    for rep in range(2):  # the first pass warms up; the second is reported
-        sq.zero_()
-        kern = []
-        for c0 in range(0, Ktot, C):
-            synth.fill(x, C, P, seed=seed + 7, k0=c0)  # refill = ingress stand-in, not timed
-            kern += _timed(lambda: kx.qfed_accumulate(x, C, P, last=last, alpha=alpha[c0:c0 + C], lr=lr,
-                                                      delta=delta, sqnorm=sq[c0:c0 + C], workspace=ws,
-                                                      accumulate=c0 > 0), 1, stream)
-
-        def finish():
-            kx.qfed_hs(sq, c1, c2, Ktot, hs)
-            kx.qfed_finalize(last, delta, hs, new, P)
-
-        kern += _timed(finish, 1, stream)
-    ms = float(sum(kern))
-    alg = 4 * Ktot * P + 8 * P + 8 * Ktot  # SURVEY §8d q-FedAvg: 4KP + 4P (last) + 4P (new) + 8K
-    out["c5_qfedavg_shard_k10000_p12500000_streamed"] = {
-        "clients": Ktot, "params_per_gpu": P, "chunk": C, "of": "10000 x 100M q-FedAvg over 8 GPUs",
-        "round_kernel_ms": ms, "client_updates_per_s": Ktot / (ms * 1e-3), "hbm_gbps": alg / (ms * 1e-3) / 1e9,
-        "note": "staging refills (ingress stand-in) excluded; all round kernels timed with HIP events"}
-    del x
-    torch.cuda.empty_cache()
+def single_gpu_configs(dev, seed, shards, backend, cpu_budget) -> dict:
+    """N = 1: BASELINE configs 1-5 on this GPU, each beside its CPU leg (the oracle on this host)."""
+    out = {"c1_femnist_cnn_k10_host_round": c1_host_round(dev, seed)}
+    c2 = config_line("c2", CONFIGS["c2"], dev, 0, 1, shards, seed, backend, steps=20, warmup=4, sets=2)
+    c2["note"] = "two rotating input sets (400 MB each): the 256 MiB Infinity Cache cannot serve repeats"
+    out["c2_synthetic_k100_p1M"] = c2
+    out["c3_resnet18_layout_k1000_p11191242"] = config_line("c3", CONFIGS["c3"], dev, 0, 1, shards, seed, backend,
+                                                            steps=10, warmup=2)
+    out["c4_fedyogi_k1000_p25M"] = config_line("c4", CONFIGS["c4"], dev, 0, 1, shards, seed, backend)
+    out["c5_qfedavg_k10000_p100M"] = config_line("c5", CONFIGS["c5"], dev, 0, 1, shards, seed, backend, steps=2,
+                                                 warmup=1)
+    # one GPU's share of the multi-GPU configs at their BASELINE GPU counts
+    out["c4_fedyogi_shard_of_4"] = config_line(
+        "c4s", dict(CONFIGS["c4"], params=25_000_000 // 4), dev, 0, 1, shards, seed, backend, steps=10)
+    out["c5_qfedavg_shard_of_8"] = config_line(
+        "c5s", dict(CONFIGS["c5"], params=100_000_000 // 8), dev, 0, 1, shards, seed, backend, steps=3, warmup=1)
+    if cpu_budget > 0:
+        out["c1_femnist_cnn_k10_host_round"]["cpu_baseline"] = cpu_baseline_c1(seed)
+        for key, name, share in (("c2_synthetic_k100_p1M", "c2", 0.1), ("c3_resnet18_layout_k1000_p11191242", "c3", 0.4),
+                                 ("c4_fedyogi_k1000_p25M", "c4", 0.8), ("c5_qfedavg_k10000_p100M", "c5", 1.0)):
+            c = CONFIGS[name]
+            leg = cpu_leg(c["policy"], c["clients"], c["params"], cpu_budget * share, seed)
+            leg["device_speedup"] = out[key]["client_updates_per_s"] / leg["client_updates_per_s"]
+            out[key]["cpu_baseline"] = leg
     return out
 
 
@@ -312,174 +513,92 @@ def main():
     from fedscale_amd.state import ShardGroup
 
     shards = ShardGroup(rank, world, mode=args.shard)
-    cmode = shards.shards_clients
-
-    from fedscale_amd import kernels as kx
-    from fedscale_amd import synth
-    from fedscale_amd.bucket import round_up
-
-    K, P = args.clients, args.params
-    ld = round_up(P, 64)
-    x = torch.empty(K, ld, dtype=torch.float32, device=dev)
-    synth.fill(x, K, P, seed=args.seed + 7919 * rank)
-    out = torch.zeros(ld, dtype=torch.float32, device=dev)
-    acc = torch.zeros(ld, dtype=torch.float32, device=dev) if cmode else None  # client mode: partial chain
-    Kg = K * world if cmode else K  # clients in the round (client mode: every rank brings K)
-    denom = float(np.float32(Kg))
-    yogi = None
-    if args.policy == "fedyogi":
-        yogi = dict(last=torch.zeros(ld, device=dev), m=torch.zeros(ld, device=dev), v=torch.zeros(ld, device=dev),
-                    eta=float(np.float32(3e-3)), tau=float(np.float32(1e-8)), beta=float(np.float32(0.9)),
-                    omb=float(np.float32(1 - 0.9)), omb2=float(np.float32(1 - 0.99)), init=False)
-        synth.fill(yogi["last"].view(1, -1), 1, P, seed=args.seed + 1)
-    a = None
-    if args.policy == "fedbuff":
-        s = [1 / (1 + (k % 6)) ** 0.5 for k in range(Kg)]
-        a = torch.tensor(np.asarray(s[rank * K:(rank + 1) * K] if cmode else s, dtype=np.float32), device=dev)
-        denom = float(np.float32(sum(s)))
-    gathered = None
-    qf = None
-    if args.policy == "qfedavg":
-        if K > kx.qfed_max_chunk():
-            raise SystemExit(f"--policy qfedavg: K <= {kx.qfed_max_chunk()} per chunk in this bench")
-        rng = np.random.default_rng(args.seed)
-        losses = rng.uniform(0.5, 2.0, size=Kg)
-        lr, q = 0.05, 1.0
-        mine = losses[rank * K:(rank + 1) * K] if cmode else losses
-        qf = dict(last=torch.empty(1, ld, device=dev), delta=torch.zeros(ld, device=dev),
-                  sq=torch.zeros(Kg, dtype=torch.float64, device=dev), ws=kx.qfed_workspace(K, dev),
-                  hs=torch.zeros(2, device=dev), lr=lr,
-                  alpha=torch.tensor([np.float32(np.float_power(l + 1e-10, q)) for l in mine], device=dev),
-                  c1=torch.tensor([np.float32(q * np.float_power(l + 1e-10, q - 1)) for l in losses], device=dev),
-                  c2=torch.tensor([np.float32((1 / lr) * np.float_power(l + 1e-10, q)) for l in losses], device=dev))
-        synth.fill(qf["last"], 1, P, seed=args.seed + (0 if cmode else 7919 * rank), scale_noise=0.0)
-        qf["last"] = qf["last"][0]
-
-    stream = torch.cuda.current_stream(dev)
-
-    def step(ev=None):
-        if ev is not None:
-            ev[0].record(stream)
-        if qf is not None:  # optimizers.py:73-104: phase 1 (timed as the dominant kernel), hs, phase 2
-            qf["sq"].zero_()
-            k0 = rank * K if cmode else 0
-            kx.qfed_accumulate(x, K, P, last=qf["last"], alpha=qf["alpha"], lr=qf["lr"], delta=qf["delta"],
-                               sqnorm=qf["sq"][k0:k0 + K], workspace=qf["ws"], accumulate=False)
-            if ev is not None:
-                ev[1].record(stream)
-            if cmode:  # per-rank partial delta chains + each client's norm from its owner rank
-                shards.all_reduce_sum(qf["delta"])
-                shards.all_reduce_sum(qf["sq"])
-            elif world > 1:
-                shards.all_reduce_sum(qf["sq"])
-            kx.qfed_hs(qf["sq"], qf["c1"], qf["c2"], Kg, qf["hs"])
-            kx.qfed_finalize(qf["last"], qf["delta"], qf["hs"], out, P)
-            return
-        if cmode:  # partial chain of this rank's clients, RCCL all-reduce, finish on the summed vector
-            kx.reduce(x, K, P, acc, a=a)
-            if ev is not None:
-                ev[1].record(stream)
-            shards.all_reduce_sum(acc)
-            if yogi is None:
-                kx.reduce(acc.view(1, ld), 1, P, out, denom=denom, finalize=True)
-            else:
-                kx.reduce_yogi(acc.view(1, ld), 1, P, out=out, denom=denom, **yogi)
-            return
-        if yogi is None:
-            kx.reduce(x, K, P, out, a=a, denom=denom, finalize=True)
-        else:
-            kx.reduce_yogi(x, K, P, out=out, denom=denom, **yogi)
-        if ev is not None:
-            ev[1].record(stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(evs[i])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    cfg = args.cfg
+    policy, K, P = cfg["policy"], cfg["clients"], cfg["params"]
+    weak = args.scaling == "weak"
+    w = Workload(policy, K, P, rank, world, dev, args.seed, shards, weak=weak)
+    (wall, kern_ms_max), kern_ms = time_workload(w, args.steps, args.warmup, dev, world, args.dist_backend)
+    strong = not weak and not w.cmode
 
     reassembly_ms = None
-    if args.reassemble and world > 1:
-        shards.all_gather(out)  # warm the communicator
-        torch.cuda.synchronize(dev)
-        dist.barrier()
+    if world > 1 and not args.no_reassemble and not w.cmode:  # egress: rebuild the global model (RCCL)
+        shards.collective_all_gather(w.out)  # warm the communicator
+        _sync_all(dev, world)
         t0r = time.perf_counter()
         for _ in range(5):
-            gathered = shards.all_gather(out)
+            shards.collective_all_gather(w.out)
         torch.cuda.synchronize(dev)
-        reassembly_ms = (time.perf_counter() - t0r) * 1e3 / 5
+        reassembly_ms = _max_over_ranks([(time.perf_counter() - t0r) * 1e3 / 5], dev, world, args.dist_backend)[0]
+    alg_bytes = w.alg_bytes
+    P_local, n_passes = w.P, len(w.passes)
+    w.free()
+    del w
 
-    t = torch.tensor([wall, kern_ms], dtype=torch.float64)
-    if world > 1:
-        if args.dist_backend == "nccl":
-            t = t.to(dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall, kern_ms_max = float(t[0]), float(t[1])
+    other = None
+    if not args.no_other_configs and args.config == "headline":
+        if world == 1:
+            other = single_gpu_configs(dev, args.seed, shards, args.dist_backend, args.cpu_seconds)
+        elif not shards.shards_clients:  # configs 4 and 5 at N GPUs (the driver's 4- and 8-GPU runs)
+            other = {
+                f"c4_fedyogi_k1000_p25M_x{world}": config_line(
+                    "c4", CONFIGS["c4"], dev, rank, world, shards, args.seed, args.dist_backend),
+                f"c5_qfedavg_k10000_p100M_x{world}": config_line(
+                    "c5", CONFIGS["c5"], dev, rank, world, shards, args.seed, args.dist_backend, steps=2, warmup=1)}
 
     if rank == 0:
         ms_per_step = wall * 1e3 / args.steps
-        value = world * K * args.steps / wall
-        extra = {"fedavg": 0, "fedbuff": 4 * K, "fedyogi": 0 if cmode else 20 * P,
-                 "qfedavg": 4 * P + 8 * K}[args.policy]
-        alg_bytes = 4 * K * P + 4 * P + extra  # SURVEY §8d algorithmic bytes per launch (per GPU)
+        value = (K if strong else world * K) * args.steps / wall
         achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
         traffic = None
         if os.path.exists(PMC_FILE):
             try:
                 pmc = json.load(open(PMC_FILE))
-                key = f"{args.policy}_k{K}_p{P}"
+                key = f"{policy}_k{K}_p{P_local}"
                 if key in pmc:
                     traffic = pmc[key]["hbm_bytes_per_launch"]
             except Exception:
                 traffic = None
+        w_cmode = shards.shards_clients
+        if w_cmode:
+            config = {"workload": f"{policy}_k{K}_per_gpu_p{P}_clientshard", "clients": K * world,
+                      "clients_per_gpu": K, "params": P, "model_params_total": P, "policy": policy,
+                      "parallelism": f"client-shard x{world} + RCCL all-reduce (one process per GPU)"}
+        elif world == 1 or weak:
+            config = {"workload": f"{policy}_k{K}_p{P}_per_gpu", "clients": K, "params_per_gpu": P,
+                      "model_params_total": P * world, "policy": policy,
+                      "parallelism": f"param-shard x{world} (one process per GPU)"}
+        else:
+            config = {"workload": f"{policy}_k{K}_p{P}_sharded_x{world}", "clients": K, "params_per_gpu": P_local,
+                      "model_params_total": P, "policy": policy,
+                      "parallelism": f"param-shard x{world} (one process per GPU, no data-path collective)"}
+        if n_passes > 1:
+            config["streamed_passes"] = n_passes
         res = {
             "metric": ("client-updates/sec + HBM GB/s, device-resident FedAvg reduce of KxP fp32"
-                       if args.policy == "fedavg" else
-                       f"client-updates/sec + HBM GB/s, device-resident {args.policy} round of KxP fp32"),
+                       if policy == "fedavg" else
+                       f"client-updates/sec + HBM GB/s, device-resident {policy} round of KxP fp32"),
             "value": value, "unit": "client-updates/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32",
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic full-weight client updates (base + noise, hash-generated on device), HBM-resident",
-            "config": ({"workload": f"{args.policy}_k{K}_p{P}_per_gpu", "clients": K, "params_per_gpu": P,
-                        "model_params_total": P * world, "policy": args.policy,
-                        "parallelism": f"param-shard x{world} (one process per GPU)"} if not cmode else
-                       {"workload": f"{args.policy}_k{K}_per_gpu_p{P}_clientshard", "clients": Kg,
-                        "clients_per_gpu": K, "params": P, "model_params_total": P, "policy": args.policy,
-                        "parallelism": f"client-shard x{world} + RCCL all-reduce (one process per GPU)"}),
+            "config": config,
             "hbm_gbps": achieved,
             "kernel_ms": kern_ms,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": ("k_qfed_accum + k_qfed_gather (fa_qfed_accumulate)" if args.policy == "qfedavg"
-                                    else "k_reduce (fa_reduce, this rank's partial chain)" if cmode else
+                         "kernel": ("k_qfed_accum + k_qfed_gather (fa_qfed_accumulate)" if policy == "qfedavg"
+                                    else "k_reduce (fa_reduce, this rank's partial chain)" if w_cmode else
                                     {"fedavg": "k_reduce (fa_reduce FA_FINALIZE)",
                                      "fedbuff": "k_reduce weighted (fa_reduce FA_FINALIZE)",
-                                     "fedyogi": "k_reduce EPI_YOGI (fa_reduce_yogi)"}[args.policy]),
+                                     "fedyogi": "k_reduce EPI_YOGI (fa_reduce_yogi)"}[policy]),
                          "alg_bytes_per_launch": alg_bytes},
         }
         if reassembly_ms is not None:
             res["reassembly_ms"] = reassembly_ms
-        if world == 1 and not args.no_other_configs:
-            del x
-            torch.cuda.empty_cache()
-            res["other_configs"] = other_configs(dev, args.seed)
+        if other is not None:
+            res["other_configs"] = other
         if world == 1 and args.cpu_seconds > 0:
-            x = None
-            torch.cuda.empty_cache()
             res["cpu_baseline"] = cpu_baseline(K, P, args.cpu_seconds, args.seed)
-            if "other_configs" in res:  # the oracle on config 1's round, beside the device round
-                res["other_configs"]["c1_femnist_cnn_k10_host_round"]["cpu_baseline"] = cpu_baseline_c1(args.seed)
         else:
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
