@@ -41,7 +41,7 @@ SIGNATURES = {
     "fa_qfed_max_chunk": (_i32, []),
     "fa_qfed_workspace_bytes": (_i64, [_i32]),
     "fa_qfed_accumulate": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p,
-                                  _c_void_p, _i32, _c_void_p]),
+                                  _c_void_p, _c_void_p, _i32, _c_void_p]),
     "fa_qfed_hs": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p]),
     "fa_qfed_finalize": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p]),
     "fa_side_accumulate": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _i32,

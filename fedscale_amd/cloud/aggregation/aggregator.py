@@ -34,11 +34,32 @@ class _Decoded:
         self.value = value
 
 
+class StagedUpload:
+    """What a retained q-FedAvg result holds in place of ``update_weight`` once the upload is staged in HBM
+    (``device_release_uploads``): the device round is the only consumer, so the host arrays are let go."""
+
+    __slots__ = ("arrival",)
+
+    def __init__(self, arrival: int):
+        self.arrival = arrival
+
+    def __repr__(self):
+        return f"<update {self.arrival} of this round, staged in HBM>"
+
+
 class DeviceAggregatorMixin:
     #: clients staged per chunk (None: as many as fit in half of the free HBM)
     device_round_capacity = None
-    #: keep the FedAvg mean as ``model_weights`` in fused fed-yogi rounds (costs P*4 bytes of writes)
+    #: keep the FedAvg mean as ``model_weights`` (aggregator.py:505-507): fed-yogi rounds write it in the
+    #: fused pass (P*4 bytes); q-FedAvg rounds that span several staging chunks fuse the FedAvg chain into
+    #: their phase-1 kernel (measured 9 % of it), single-chunk ones recompute it from the staged updates
+    #: when model_weights is read; "always" fuses the chain in every q-FedAvg round (the mean then survives
+    #: the next round's reuse of the staging); False keeps no mean
     device_keep_mean = True
+    #: drop the retained q-FedAvg results' ``update_weight`` (aggregator.py:466-467) once it is staged in
+    #: HBM: the device round never reads it again, and with zero-copy ingress each retained array would
+    #: pin its whole upload payload in host memory (45 GB for 1000 ResNet-18 uploads)
+    device_release_uploads = True
     #: unpickle executor payloads without copying their arrays (fedscale_amd/ingress.py); the arrays of
     #: ``update_weight`` are then read-only views of the payload
     device_zero_copy_ingress = True
@@ -218,12 +239,14 @@ class DeviceAggregatorMixin:
         w = self._wrapper()
         if self._is_first_result_in_round() or self._device_round is None:
             self._device_round = w.begin_round(self.tasks_round, self._device_policy(),
-                                               capacity=self.device_round_capacity)
+                                               capacity=self.device_round_capacity, keep_mean=self.device_keep_mean)
         rnd = self._device_round
         if rnd.policy == "qfedavg":
             a = w.optimizer.args  # optimizers.py:69 reads the live args at step time
             rnd.add(results["update_weight"], loss=results["moving_loss"], learning_rate=a.learning_rate,
                     q=a.qfed_q)
+            if self.device_release_uploads:
+                results["update_weight"] = StagedUpload(rnd.n - 1)
         else:
             rnd.add(results["update_weight"])
         if self._is_last_result_in_round():

@@ -105,7 +105,7 @@ class ShardedModelAdapter(TorchModelAdapter):
         return row
 
     # ---- rounds -----------------------------------------------------------------------------------
-    def begin_round(self, K: int, policy: str, capacity: Optional[int] = None) -> ShardedRound:
+    def begin_round(self, K: int, policy: str, capacity: Optional[int] = None, keep_mean=True) -> ShardedRound:
         cap = capacity or self.staging_capacity
         if not cap:  # one capacity for all parts, so they fold their chunks in step; parts sharing a
             # device share its budget (half of the free HBM)
@@ -114,7 +114,7 @@ class ShardedModelAdapter(TorchModelAdapter):
                 per_dev[p.device] = per_dev.get(p.device, 0) + 1
             cap = min(default_capacity(p.layout, K, p.device, budget_fraction=0.5 / per_dev[p.device])
                       for p in self.parts)
-        return ShardedRound(self, [p.begin_round(K, policy, capacity=cap) for p in self.parts])
+        return ShardedRound(self, [p.begin_round(K, policy, capacity=cap, keep_mean=keep_mean) for p in self.parts])
 
     def apply_round(self, rnd: ShardedRound, denom32: float, denom64: float, client_training_results=None,
                     keep_mean: bool = True):

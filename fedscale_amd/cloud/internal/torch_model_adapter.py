@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from ...bucket import BucketLayout, ClientStaging
+from ...kernels import qfed_max_chunk as kx_qfed_max_chunk
 from ...round import DeviceRound, default_capacity
 from ...state import FlatState, ShardGroup
 from .model_adapter_base import ModelAdapterBase
@@ -323,20 +324,26 @@ class TorchModelAdapter(ModelAdapterBase):
         return (self.__class__, (self.get_model(), self.optimizer))
 
     # ---- device fast path -----------------------------------------------------------------------
-    def begin_round(self, K: int, policy: str, capacity: Optional[int] = None) -> DeviceRound:
+    def begin_round(self, K: int, policy: str, capacity: Optional[int] = None, keep_mean=True) -> DeviceRound:
+        """``keep_mean`` for q-FedAvg rounds: True fuses the FedAvg chain when the round spans several chunks
+        (the staged updates are then gone by the end of the round), "always" in every round (the mean is then
+        independent of the staging's later reuse), False never (model_weights of such rounds raises)."""
         cap = capacity or self.staging_capacity
         K_local = K
         if self.shards.shards_clients:  # this rank stages only its block of the arrivals
             k0, k1 = self.shards.client_block(K)
             K_local = max(1, k1 - k0)
         want = min(cap or default_capacity(self.layout, K_local, self.device), K_local)
+        if policy == "qfedavg":  # phase-1 chunks hold at most fa_qfed_max_chunk() clients
+            want = min(want, kx_qfed_max_chunk())
         if self.staging is None or self.staging.capacity < want:
             self.staging = None
             self.staging = ClientStaging(self.layout, self.device, want)
         snap = self._snapshot()
+        chain = keep_mean == "always" or (bool(keep_mean) and want < K_local)
         return DeviceRound(self.layout, self.device, K, policy, capacity=want, staging=self.staging,
                            last_f32=snap.f32, last_i64=snap.side,
-                           clients=self.shards if self.shards.shards_clients else None)
+                           clients=self.shards if self.shards.shards_clients else None, mean_chain=chain)
 
     def apply_round(self, rnd: DeviceRound, denom32: float, denom64: float, client_training_results=None,
                     keep_mean: bool = True):

@@ -493,6 +493,7 @@ struct QfArgs {
   int fast;       // 0: lr outside [2^-20, 2^20] -> IEEE division for every element
   int sw;         // strips (64 f4 columns) per wave per tile, <= QF_V
   float* delta;
+  float* chain;  // CHAIN: the plain FedAvg chain of the same rows (aggregator.py:500-503)
   double* part;  // [gridDim.x][K]
 };
 
@@ -566,7 +567,7 @@ __device__ __forceinline__ f4 rows_load(__amdgpu_buffer_rsrc_t r, uint32_t voff)
 #define QF_PIPE 0  // 1: software-pipelined client loads (two row buffers); measured slower, see DESIGN.md
 #endif
 // WIDE: one descriptor spans all QF_G rows of a group (QF_G rows < 4 GiB); otherwise one per QF_U rows.
-template <bool WIDE>
+template <bool WIDE, bool CHAIN>
 __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
   __shared__ double sq[4][QF_MAXK];
   const int lane = threadIdx.x & 63;
@@ -586,7 +587,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
     const int64_t sw0 = tile * 4 * sw + (int64_t)wave * sw;  // this wave's first strip
     const int64_t c0 = sw0 * 64 + lane;
     bool ok[QF_V];
-    f4 L[QF_V], D[QF_V];
+    f4 L[QF_V], D[QF_V], C[QF_V];
     uint32_t voff[QF_V];  // byte offset of this lane's column j in a row, or QF_OOB
 #pragma unroll
     for (int j = 0; j < QF_V; ++j) {
@@ -595,6 +596,9 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       L[j] = ok[j] ? reinterpret_cast<const f4*>(q.last)[c0 + 64 * j] : f4{0.f, 0.f, 0.f, 0.f};
       D[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.delta)[c0 + 64 * j]
                                                   : f4{0.f, 0.f, 0.f, 0.f};
+      if (CHAIN)
+        C[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.chain)[c0 + 64 * j]
+                                                    : f4{0.f, 0.f, 0.f, 0.f};
     }
 #if QF_PIPE
     // row slice of client k (k >= K: an empty range, the loads return zeros and touch no memory)
@@ -623,6 +627,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       DivRange rng;
 #pragma unroll
       for (int j = 0; j < QF_V; ++j) {
+        if (CHAIN) C[j] = first ? t[j] : C[j] + t[j];  // the FedAvg chain of the same upload
         t[j] = L[j] - t[j];  // (last - W), optimizers.py:83; the "* 1.0" is exact
         g[j].x = fast_div(t[j].x, q.lr, q.rlr);
         g[j].y = fast_div(t[j].y, q.lr, q.rlr);
@@ -760,12 +765,206 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
     }
 #pragma unroll
     for (int j = 0; j < QF_V; ++j)
-      if (ok[j]) reinterpret_cast<f4*>(q.delta)[c0 + 64 * j] = D[j];
+      if (ok[j]) {
+        reinterpret_cast<f4*>(q.delta)[c0 + 64 * j] = D[j];
+        if (CHAIN) reinterpret_cast<f4*>(q.chain)[c0 + 64 * j] = C[j];
+      }
   }
   __syncthreads();
   for (int k = threadIdx.x; k < q.K; k += 256)
     q.part[(int64_t)blockIdx.x * q.K + k] = ((sq[0][k] + sq[1][k]) + sq[2][k]) + sq[3][k];
 }
+
+// ------------------------------------------------------------------------------------------------
+// q-FedAvg phase 1, second design (the default, QF_KERNEL 2): 2 waves per SIMD, the FedAvg chain fused
+// ------------------------------------------------------------------------------------------------
+// The first design (k_qfed_accum above) runs 1 wave per SIMD: `last`, the delta chain, the loaded row and
+// the quotients all live in registers (256 VGPRs + AGPR parking), so a wave has no loads in flight while
+// it computes (~20 % of its time) and the kernel reads HBM at 0.83 of peak.  Here:
+//  * the wave's `last` tile lives in LDS (written and read back by the same lane: no barrier), 16 KiB per
+//    wave, 8 waves = 128 KiB per workgroup, one workgroup per CU;
+//  * per client, pass 1 forms a = last - W in place of the loaded row and folds the range test of the
+//    constant-divisor division; the wave votes; pass 2 divides (fast or IEEE for the whole client),
+//    squares and extends the delta chain — no quotient array, so t, D (and the FedAvg chain C) fit in
+//    < 256 VGPRs: 2 waves per SIMD cover each other's compute phases with their loads;
+//  * CHAIN: the plain FedAvg chain C += W (aggregator.py:500-503) rides along (+1 add per element and
+//    +8P bytes per chunk), so the reference's model_weights (the mean, :505-507) exists for any K;
+//  * per-client partial squared norms: each (workgroup, wave) owns a row of K fp64 in the workspace and
+//    accumulates its tiles into it in tile order (read-add-write, the read issued ahead of the group's
+//    loads); k_qfed_gather2a/b then sum the 2048 rows in a fixed two-level order.  No atomics, so the
+//    result is the same bits on every run and every device.
+#ifndef QF_KERNEL
+#define QF_KERNEL 1  // the no-chain launches (profiles/r02_tune_qfed2.log: the 1-wave design reads faster)
+#endif
+#ifndef QF2_WAVES
+#define QF2_WAVES 8
+#endif
+#ifndef QF2_V
+#define QF2_V 16
+#endif
+#ifndef QF2_GRID
+#define QF2_GRID 256
+#endif
+#define QF2_SEG 32  // first-level segments of the norm gather
+#define QF2_ROWS (QF2_GRID * QF2_WAVES)
+
+struct Qf2Args {
+  const float* x;
+  int64_t ld4, P4;
+  int K;
+  int flags;
+  const float* last;
+  const float* alpha;
+  float lr, rlr;
+  int fast;
+  int sw;  // strips (64 f4 columns) per wave per tile, <= QF2_V
+  float* delta;
+  float* chain;
+  double* part;  // [QF2_ROWS][K]
+};
+
+template <bool CHAIN>
+__global__ __launch_bounds__(64 * QF2_WAVES, 1) void k_qfed_accum2(Qf2Args q) {
+  __shared__ f4 Ls[QF2_WAVES * QF2_V * 64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  f4* myL = Ls + wave * (QF2_V * 64) + lane;  // slot j at myL[64 * j]: this lane's own bytes
+  const int64_t S = (q.P4 + 63) / 64;
+  const int sw = q.sw;
+  const int64_t ntiles = (S + (int64_t)QF2_WAVES * sw - 1) / ((int64_t)QF2_WAVES * sw);
+  const uint32_t rowbytes = (uint32_t)(q.P4 * 16);
+  const bool acc_in = (q.flags & FA_ACCUMULATE) != 0;
+  double* prow = q.part + ((int64_t)blockIdx.x * QF2_WAVES + wave) * q.K;
+  const int jcl = (lane >> 4) & 3;           // the client whose wave total this lane ends up with
+  const bool writer = (lane & 15) == 0;
+  const f4 z4 = f4{0.f, 0.f, 0.f, 0.f};
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const bool first_tile = tile == (int64_t)blockIdx.x;
+    const int64_t c0 = (tile * QF2_WAVES + wave) * sw * 64 + lane;
+    uint32_t voff[QF2_V];
+    f4 D[QF2_V], C[QF2_V];
+#pragma unroll
+    for (int j = 0; j < QF2_V; ++j) {
+      const bool ok = j < sw && c0 + 64 * j < q.P4;
+      voff[j] = ok ? (uint32_t)((c0 + 64 * j) * 16) : QF_OOB;
+      myL[64 * j] = ok ? reinterpret_cast<const f4*>(q.last)[c0 + 64 * j] : z4;
+      D[j] = (ok && acc_in) ? reinterpret_cast<const f4*>(q.delta)[c0 + 64 * j] : z4;
+      if (CHAIN) C[j] = (ok && acc_in) ? reinterpret_cast<const f4*>(q.chain)[c0 + 64 * j] : z4;
+    }
+    for (int kg = 0; kg < q.K; kg += 4) {
+      // this (workgroup, wave) row's running norms of the group's clients, from the earlier tiles
+      double old = 0.0;
+      if (!first_tile && writer && kg + jcl < q.K) old = prow[kg + jcl];
+      double v0 = 0.0, v1 = 0.0, v2 = 0.0, v3 = 0.0;
+      // not unrolled: one client's row slice in registers at a time (an unrolled loop lets the scheduler
+      // hoist the next client's 16 loads and spill)
+      const int un = q.K - kg < 4 ? q.K - kg : 4;
+#pragma unroll 1
+      for (int u = 0; u < un; ++u) {
+        const int k = kg + u;
+        // compiler barrier: the `last` tile is re-read from LDS for every client (hoisting those reads out
+        // of the loop would put the tile back into 64 VGPRs and halve the occupancy)
+        asm volatile("" ::: "memory");
+        const __amdgpu_buffer_rsrc_t rr = rows_rsrc(q.x + (int64_t)k * q.ld4 * 4, rowbytes);
+        f4 t[QF2_V];
+#pragma unroll
+        for (int j = 0; j < QF2_V; ++j) t[j] = rows_load(rr, voff[j]);
+        const bool first = (k == 0) && !acc_in;
+        DivRange rng;
+#pragma unroll
+        for (int j = 0; j < QF2_V; ++j) {  // pass 1: the FedAvg chain, a = last - W, the range test
+          if (CHAIN) C[j] = first ? t[j] : C[j] + t[j];
+          t[j] = myL[64 * j] - t[j];  // (last - W), optimizers.py:83; the "* 1.0" is exact
+          rng.add(t[j].x);
+          rng.add(t[j].y);
+          rng.add(t[j].z);
+          rng.add(t[j].w);
+        }
+        const float al = q.alpha[k];
+        double acc = 0.0;
+        if (q.fast && __all(rng.ok())) {  // pass 2: divide, square, extend the delta chain
+#pragma unroll
+          for (int j = 0; j < QF2_V; ++j) {
+            f4 g;
+            g.x = fast_div(t[j].x, q.lr, q.rlr);
+            g.y = fast_div(t[j].y, q.lr, q.rlr);
+            g.z = fast_div(t[j].z, q.lr, q.rlr);
+            g.w = fast_div(t[j].w, q.lr, q.rlr);
+            const f4 g2 = g * g;                             // torch.square(grad), fp32
+            acc += (double)((g2.x + g2.y) + (g2.z + g2.w));  // 4-term fp32 partial, then fp64
+            const f4 term = al * g;                          // float_power(...) * grad (fp32 product)
+            D[j] = first ? term : D[j] + term;
+          }
+        } else {  // rare: the whole client with the IEEE division
+#pragma unroll
+          for (int j = 0; j < QF2_V; ++j) {
+            f4 g;
+            g.x = __fdiv_rn(t[j].x, q.lr);
+            g.y = __fdiv_rn(t[j].y, q.lr);
+            g.z = __fdiv_rn(t[j].z, q.lr);
+            g.w = __fdiv_rn(t[j].w, q.lr);
+            const f4 g2 = g * g;
+            acc += (double)((g2.x + g2.y) + (g2.z + g2.w));
+            const f4 term = al * g;
+            D[j] = first ? term : D[j] + term;
+          }
+        }
+        v0 = u == 0 ? acc : v0;
+        v1 = u == 1 ? acc : v1;
+        v2 = u == 2 ? acc : v2;
+        v3 = u == 3 ? acc : v3;
+      }
+      // multi-reduce: lane l ends with the wave total of client kg + ((l >> 4) & 3)
+      double y;
+      {
+        const double v[4] = {v0, v1, v2, v3};
+        const bool b5 = lane & 32, b4 = lane & 16;
+        double w2[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const double keep = b5 ? v[i + 2] : v[i], send = b5 ? v[i] : v[i + 2];
+          w2[i] = keep + shfl_xor_d(send, 32);
+        }
+        const double keep = b4 ? w2[1] : w2[0], send = b4 ? w2[0] : w2[1];
+        y = keep + shfl_xor_d(send, 16);
+        y += shfl_xor_d(y, 8);
+        y += shfl_xor_d(y, 4);
+        y += shfl_xor_d(y, 2);
+        y += shfl_xor_d(y, 1);
+      }
+      if (writer && kg + jcl < q.K) prow[kg + jcl] = first_tile ? y : old + y;
+    }
+#pragma unroll
+    for (int j = 0; j < QF2_V; ++j) {
+      if (voff[j] == QF_OOB) continue;
+      reinterpret_cast<f4*>(q.delta)[c0 + 64 * j] = D[j];
+      if (CHAIN) reinterpret_cast<f4*>(q.chain)[c0 + 64 * j] = C[j];
+    }
+  }
+  // rows of waves that owned no tile at all (tiny P) must still be defined
+  if ((int64_t)blockIdx.x >= ntiles)
+    for (int k = lane; k < q.K; k += 64) prow[k] = 0.0;
+}
+
+// first level: segment s of the QF2_ROWS partial rows -> seg[s][k]; second: sqnorm[k] += sum_s seg[s][k]
+__global__ __launch_bounds__(256) void k_qfed_gather2a(const double* __restrict__ part, int K, double* seg) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  constexpr int rps = QF2_ROWS / QF2_SEG;
+  const double* p = part + (int64_t)blockIdx.y * rps * K + k;
+  double s = 0.0;
+#pragma unroll 8
+  for (int r = 0; r < rps; ++r) s += p[(int64_t)r * K];
+  seg[(int64_t)blockIdx.y * K + k] = s;
+}
+__global__ __launch_bounds__(256) void k_qfed_gather2b(const double* __restrict__ seg, int K, double* sqnorm) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  double s = 0.0;
+  for (int i = 0; i < QF2_SEG; ++i) s += seg[(int64_t)i * K + k];
+  sqnorm[k] += s;
+}
+static_assert(QF2_ROWS % QF2_SEG == 0, "gather segments must divide the partial rows");
 
 __global__ __launch_bounds__(256) void k_qfed_gather(const double* __restrict__ part, int nblk, int K,
                                                      double* sqnorm) {
@@ -777,23 +976,23 @@ __global__ __launch_bounds__(256) void k_qfed_gather(const double* __restrict__ 
 }
 
 extern "C" int fa_qfed_max_chunk(void) { return QF_MAXK; }
-extern "C" int64_t fa_qfed_workspace_bytes(int32_t K) { return (int64_t)QF_GRID * (K > 0 ? K : 1) * 8; }
+extern "C" int64_t fa_qfed_workspace_bytes(int32_t K) {  // enough for either kernel family
+  const int64_t k = K > 0 ? K : 1;
+  const int64_t w1 = (int64_t)QF_GRID * k * 8, w2 = ((int64_t)QF2_ROWS + QF2_SEG) * k * 8;
+  return w1 > w2 ? w1 : w2;
+}
 
-extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t P, const float* last,
-                                  const float* alpha, float lr, float* delta, double* sqnorm, void* workspace,
-                                  int32_t flags, fa_stream_t stream) {
-  if (K <= 0 || K > QF_MAXK) return fail(FA_E_RANGE, "fa_qfed_accumulate: K=%d outside [1, %d]", (int)K, QF_MAXK);
-  if (P < 0 || ld < P || ld % 4) return fail(FA_E_ARG, "fa_qfed_accumulate: bad P/ld");
-  if (!x || !last || !alpha || !delta || !sqnorm || !workspace)
-    return fail(FA_E_ARG, "fa_qfed_accumulate: NULL pointer");
-  if (!aligned16(x) || !aligned16(last) || !aligned16(delta))
-    return fail(FA_E_ARG, "fa_qfed_accumulate: x/last/delta must be 16-byte aligned");
+#ifndef QF_CHAIN_KERNEL
+#define QF_CHAIN_KERNEL 1
+#endif
+
+static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const float* last, const float* alpha,
+                        float lr, int fast, float* delta, float* chain, double* sqnorm, void* workspace,
+                        int32_t flags, hipStream_t st) {
   QfArgs q{};
-  if (!(lr > 1e-30f && lr < 1e30f)) return fail(FA_E_ARG, "fa_qfed_accumulate: lr=%g outside (1e-30, 1e30)", (double)lr);
   q.x = x; q.ld4 = ld / 4; q.P4 = (P + 3) / 4; q.K = K; q.flags = flags; q.last = last; q.alpha = alpha;
-  q.lr = lr; q.rlr = 1.0f / lr; q.delta = delta; q.part = (double*)workspace;
-  q.fast = (lr >= 9.5367432e-07f && lr <= 1048576.f) ? 1 : 0;  // [2^-20, 2^20]
-  hipStream_t st = (hipStream_t)stream;
+  q.lr = lr; q.rlr = 1.0f / lr; q.delta = delta; q.chain = chain; q.part = (double*)workspace;
+  q.fast = fast;
   // WIDE needs QF_G rows plus the sentinel below 2^32; otherwise per-row descriptors over column
   // windows of 2^28 floats (1 GiB), one launch each; the gathers add their partial norms in order.
   const bool wide = (int64_t)ld * 4 * QF_G <= (1LL << 31);
@@ -801,7 +1000,8 @@ extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t
   for (int64_t w0 = 0; w0 < P || w0 == 0; w0 += win) {
     QfArgs qw = q;
     const int64_t pw = P - w0 < win ? P - w0 : win;
-    qw.x = x + w0; qw.last = last + w0; qw.delta = delta + w0; qw.P4 = (pw + 3) / 4;
+    qw.x = x + w0; qw.last = last + w0; qw.delta = delta + w0; qw.chain = chain ? chain + w0 : nullptr;
+    qw.P4 = (pw + 3) / 4;
     {  // rounds r = tiles per workgroup at full width; then the narrowest tile that still needs r rounds
       const int64_t S = (qw.P4 + 63) / 64;
       const int64_t r = (S + (int64_t)QF_GRID * 4 * QF_V - 1) / ((int64_t)QF_GRID * 4 * QF_V);
@@ -810,10 +1010,14 @@ extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t
       if (qw.sw < 1) qw.sw = 1;
       if (qw.sw > QF_V || !QF_BALANCE) qw.sw = QF_V;
     }
-    if (wide)
-      hipLaunchKernelGGL(k_qfed_accum<true>, dim3(QF_GRID), dim3(256), 0, st, qw);
+    if (wide && chain)
+      hipLaunchKernelGGL((k_qfed_accum<true, true>), dim3(QF_GRID), dim3(256), 0, st, qw);
+    else if (wide)
+      hipLaunchKernelGGL((k_qfed_accum<true, false>), dim3(QF_GRID), dim3(256), 0, st, qw);
+    else if (chain)
+      hipLaunchKernelGGL((k_qfed_accum<false, true>), dim3(QF_GRID), dim3(256), 0, st, qw);
     else
-      hipLaunchKernelGGL(k_qfed_accum<false>, dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<false, false>), dim3(QF_GRID), dim3(256), 0, st, qw);
     int e = check_launch("fa_qfed_accumulate");
     if (e) return e;
     hipLaunchKernelGGL(k_qfed_gather, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)workspace,
@@ -825,22 +1029,98 @@ extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t
   return FA_OK;
 }
 
-__global__ void k_qfed_hs(const double* sqnorm, const float* c1, const float* c2, int K, float* hs_out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  float hs = 0.f;  // optimizers.py:70  hs = 0.0; first `0.0 + t` is exact
-  for (int k = 0; k < K; ++k) {
-    const float s = (float)sqnorm[k];      // torch.sum(...) of fp32 -> fp32
-    const float t = c1[k] * s + c2[k];     // (q*a^(q-1)) * S + (1/lr)*a^q   — two fp32 roundings, no FMA
-    hs = hs + t;
+static int launch_qfed2(const float* x, int64_t ld, int32_t K, int64_t P, const float* last, const float* alpha,
+                        float lr, int fast, float* delta, float* chain, double* sqnorm, void* workspace,
+                        int32_t flags, hipStream_t st) {
+  // per-row descriptors: a row's num_records and the voffsets stay below 2^32 for windows of 2^28 floats
+  const int64_t win = 1LL << 28;
+  for (int64_t w0 = 0; w0 < P || w0 == 0; w0 += win) {
+    const int64_t pw = P - w0 < win ? P - w0 : win;
+    Qf2Args q{};
+    q.x = x + w0; q.ld4 = ld / 4; q.P4 = (pw + 3) / 4; q.K = K; q.flags = flags; q.last = last + w0;
+    q.alpha = alpha; q.lr = lr; q.rlr = 1.0f / lr; q.fast = fast; q.delta = delta + w0;
+    q.chain = chain ? chain + w0 : nullptr; q.part = (double*)workspace;
+    {  // rounds r = tiles per workgroup at full width; then the narrowest tile that still needs r rounds
+      const int64_t S = (q.P4 + 63) / 64;
+      const int64_t r = (S + (int64_t)QF2_ROWS * QF2_V - 1) / ((int64_t)QF2_ROWS * QF2_V);
+      const int64_t strips = r > 0 ? (S + (int64_t)QF2_GRID * r - 1) / ((int64_t)QF2_GRID * r) : 1;
+      q.sw = (int)((strips + QF2_WAVES - 1) / QF2_WAVES);
+      if (q.sw < 1) q.sw = 1;
+      if (q.sw > QF2_V) q.sw = QF2_V;
+    }
+    if (chain)
+      hipLaunchKernelGGL(k_qfed_accum2<true>, dim3(QF2_GRID), dim3(64 * QF2_WAVES), 0, st, q);
+    else
+      hipLaunchKernelGGL(k_qfed_accum2<false>, dim3(QF2_GRID), dim3(64 * QF2_WAVES), 0, st, q);
+    int e = check_launch("fa_qfed_accumulate");
+    if (e) return e;
+    double* seg = (double*)workspace + (int64_t)QF2_ROWS * K;
+    hipLaunchKernelGGL(k_qfed_gather2a, dim3((K + 255) / 256, QF2_SEG), dim3(256), 0, st, (const double*)workspace,
+                       (int)K, seg);
+    hipLaunchKernelGGL(k_qfed_gather2b, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)seg, (int)K, sqnorm);
+    e = check_launch("fa_qfed_accumulate(gather)");
+    if (e) return e;
+    if (pw >= P - w0) break;
   }
-  hs_out[0] = hs;
-  hs_out[1] = hs + 1e-10f;                 // optimizers.py:102 (hs + 1e-10)
+  return FA_OK;
+}
+
+extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t P, const float* last,
+                                  const float* alpha, float lr, float* delta, float* chain, double* sqnorm,
+                                  void* workspace, int32_t flags, fa_stream_t stream) {
+  if (K <= 0 || K > QF_MAXK) return fail(FA_E_RANGE, "fa_qfed_accumulate: K=%d outside [1, %d]", (int)K, QF_MAXK);
+  if (P < 0 || ld < P || ld % 4) return fail(FA_E_ARG, "fa_qfed_accumulate: bad P/ld");
+  if (!x || !last || !alpha || !delta || !sqnorm || !workspace)
+    return fail(FA_E_ARG, "fa_qfed_accumulate: NULL pointer");
+  if (!aligned16(x) || !aligned16(last) || !aligned16(delta) || !aligned16(chain))
+    return fail(FA_E_ARG, "fa_qfed_accumulate: x/last/delta/chain must be 16-byte aligned");
+  if (!(lr > 1e-30f && lr < 1e30f)) return fail(FA_E_ARG, "fa_qfed_accumulate: lr=%g outside (1e-30, 1e30)", (double)lr);
+  hipStream_t st = (hipStream_t)stream;
+  const int fast = (lr >= 9.5367432e-07f && lr <= 1048576.f) ? 1 : 0;  // [2^-20, 2^20]
+  const int kern = chain ? QF_CHAIN_KERNEL : QF_KERNEL;
+  if (kern == 2) return launch_qfed2(x, ld, K, P, last, alpha, lr, fast, delta, chain, sqnorm, workspace, flags, st);
+  return launch_qfed1(x, ld, K, P, last, alpha, lr, fast, delta, chain, sqnorm, workspace, flags, st);
+}
+
+// hs (optimizers.py:96-98) is a sequential fp32 sum in arrival order, so its final add chain stays on one
+// thread; everything around it is parallel: all 256 threads form the terms t_k = c1[k]*fp32(sqnorm[k]) +
+// c2[k] (two fp32 roundings, no FMA) into LDS, a slab at a time, and thread 0 adds them from LDS (the
+// loads no longer sit on the dependent chain: 10,000 clients take tens of µs instead of ~1 ms).
+#define HS_SLAB 8192
+__global__ __launch_bounds__(256) void k_qfed_hs(const double* sqnorm, const float* c1, const float* c2, int K,
+                                                 float* hs_out) {
+  __shared__ __attribute__((aligned(16))) float terms[HS_SLAB];
+  float hs = 0.f;  // optimizers.py:70  hs = 0.0; the first `0.0 + t` is exact
+  for (int k0 = 0; k0 < K; k0 += HS_SLAB) {
+    const int n = K - k0 < HS_SLAB ? K - k0 : HS_SLAB;
+    for (int i = threadIdx.x; i < n; i += 256) {
+      const float sk = (float)sqnorm[k0 + i];               // torch.sum(...) of fp32 -> fp32
+      terms[i] = c1[k0 + i] * sk + c2[k0 + i];             // (q*a^(q-1)) * S + (1/lr)*a^q
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int i = 0;
+      for (; i + 4 <= n; i += 4) {
+        const float4 t = *reinterpret_cast<const float4*>(terms + i);
+        hs = hs + t.x;
+        hs = hs + t.y;
+        hs = hs + t.z;
+        hs = hs + t.w;
+      }
+      for (; i < n; ++i) hs = hs + terms[i];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    hs_out[0] = hs;
+    hs_out[1] = hs + 1e-10f;  // optimizers.py:102 (hs + 1e-10)
+  }
 }
 
 extern "C" int fa_qfed_hs(const double* sqnorm, const float* c1, const float* c2, int32_t K, float* hs_out,
                           fa_stream_t stream) {
   if (K < 0 || !sqnorm || !c1 || !c2 || !hs_out) return fail(FA_E_ARG, "fa_qfed_hs: bad arguments");
-  hipLaunchKernelGGL(k_qfed_hs, dim3(1), dim3(64), 0, (hipStream_t)stream, sqnorm, c1, c2, (int)K, hs_out);
+  hipLaunchKernelGGL(k_qfed_hs, dim3(1), dim3(256), 0, (hipStream_t)stream, sqnorm, c1, c2, (int)K, hs_out);
   return check_launch("fa_qfed_hs");
 }
 

@@ -98,17 +98,21 @@ def qfed_workspace(K: int, device) -> torch.Tensor:
     return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
 
 
-def qfed_accumulate(x, K, P, *, last, alpha, lr, delta, sqnorm, workspace, accumulate):
+def qfed_accumulate(x, K, P, *, last, alpha, lr, delta, sqnorm, workspace, accumulate, chain=None):
+    """q-FedAvg phase 1 over one chunk (fa_qfed_accumulate); ``chain`` (optional) carries the plain FedAvg
+    sum of the same updates (the reference's model_weights before the division)."""
     ld = _check_x(x, K, P)
     _dev(last, torch.float32, "last", _cols(P))
     _dev(delta, torch.float32, "delta", _cols(P))
+    if chain is not None:
+        _dev(chain, torch.float32, "chain", _cols(P))
     _dev(alpha, torch.float32, "alpha", K, align=4)
     _dev(sqnorm, torch.float64, "sqnorm", K, align=8)
     _dev(workspace, torch.float64, "workspace")
     if workspace.numel() * 8 < N.load().fa_qfed_workspace_bytes(K):
         raise ValueError("workspace too small")
-    call("fa_qfed_accumulate", ptr(x), ld, K, P, ptr(last), ptr(alpha), float(lr), ptr(delta), ptr(sqnorm),
-         ptr(workspace), FA_ACCUMULATE if accumulate else 0, _stream(delta))
+    call("fa_qfed_accumulate", ptr(x), ld, K, P, ptr(last), ptr(alpha), float(lr), ptr(delta), ptr(chain),
+         ptr(sqnorm), ptr(workspace), FA_ACCUMULATE if accumulate else 0, _stream(delta))
 
 
 def qfed_hs(sqnorm, c1, c2, K, hs_out):

@@ -86,14 +86,17 @@ int fa_yogi_step(const float* cur, const float* last, float* m, float* v, float*
  *   g_k = (last - x[k]) / lr                      (fp32 true division)
  *   delta = FA_ACCUMULATE ? delta + alpha_k*g_0 : alpha_0*g_0; delta = delta + alpha_k*g_k ...
  *   sqnorm[k] += sum_p fp32(g_k[p]^2)              (accumulated in fp64, deterministic order)
- * Replaces: the per-client loop of optimizers.py:73-98 (client results retained at aggregator.py:466-467).
+ *   chain (optional, may be NULL) = FA_ACCUMULATE ? chain + x[0] : x[0]; chain = chain + x[k] ...
+ * Replaces: the per-client loop of optimizers.py:73-98 (client results retained at aggregator.py:466-467)
+ * and, through `chain`, the FedAvg sum the reference computes on the same inputs (aggregator.py:497-503,
+ * its model_weights): fa_reduce(chain, ld, 1, P, ..., FA_FINALIZE, denom = K) then gives the mean.
  * alpha: device fp32[K] = fp32(float_power(loss_k + 1e-10, q)).  sqnorm: device fp64[K].
  * workspace: device memory of fa_qfed_workspace_bytes(K) bytes.
  */
 int fa_qfed_max_chunk(void);
 int64_t fa_qfed_workspace_bytes(int32_t K);
 int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t P, const float* last, const float* alpha,
-                       float lr, float* delta, double* sqnorm, void* workspace, int32_t flags,
+                       float lr, float* delta, float* chain, double* sqnorm, void* workspace, int32_t flags,
                        fa_stream_t stream);
 
 /*

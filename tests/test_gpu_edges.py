@@ -45,8 +45,8 @@ def _run(names, init, K, rounds, policy=None, asynchronous=False, capacity=None,
                 else:
                     upd.append((t.numpy() + rng.normal(0, 0.01, size=tuple(t.shape))).astype(np.float32))
             res = {"client_id": k, "update_weight": upd, "moving_loss": float(rng.uniform(0.5, 2))}
+            oagg.on_result(dict(res))  # its own dict: the device path releases the staged upload in res
             agg.on_result(res)
-            oagg.on_result(res)
         yield r, dev.get_weights(), ref.get_weights()
 
 
