@@ -563,13 +563,19 @@ __device__ __forceinline__ f4 rows_load(__amdgpu_buffer_rsrc_t r, uint32_t voff)
 #ifndef QF_MINW
 #define QF_MINW 1
 #endif
-#ifndef QF_PIPE
-#define QF_PIPE 0  // 1: software-pipelined client loads (two row buffers); measured slower, see DESIGN.md
-#endif
 // WIDE: one descriptor spans all QF_G rows of a group (QF_G rows < 4 GiB); otherwise one per QF_U rows.
-template <bool WIDE, bool CHAIN>
+// GLDS > 0: the next GLDS clients' row slices stream HBM -> LDS (buffer_load_dwordx4 ... lds, no VGPR
+// destination) while the wave computes the current client from registers; at the top of each client the
+// wave copies its landed slice LDS -> registers (16 ds_read_b128) and re-arms the DMA, so loads stay in
+// flight through the compute phase at no register cost (GLDS x 16 KiB of LDS per wave).  Measured
+// (profiles/r02_tune_qfed2.log): 2-4 % SLOWER than register loads for the plain kernel, 1-5 % FASTER with
+// the fused FedAvg chain (whose 64 extra live values otherwise go through AGPRs), so chain launches use it.
+template <bool WIDE, bool CHAIN, int GLDS>
 __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
+  static_assert(GLDS == 0 || GLDS == 1 || (GLDS == 2 && QF_V == 16), "GLDS: 0, 1 or 2 LDS slices per wave");
+  constexpr int NB = GLDS > 0 ? GLDS : 1;
   __shared__ double sq[4][QF_MAXK];
+  __shared__ f4 rowbuf[GLDS > 0 ? GLDS * 4 * QF_V * 64 : 1];  // GLDS 2: 128 KiB + 32 KiB sq = 160 KiB
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < 4 * QF_MAXK; i += 256) (&sq[0][0])[i] = 0.0;
@@ -600,25 +606,6 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
         C[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.chain)[c0 + 64 * j]
                                                     : f4{0.f, 0.f, 0.f, 0.f};
     }
-#if QF_PIPE
-    // row slice of client k (k >= K: an empty range, the loads return zeros and touch no memory)
-    auto load_rows = [&](f4(&dst)[QF_V], int k) {
-      if (WIDE) {
-        const int kg = k & ~(QF_G - 1);
-        const int nr = q.K - kg;
-        const int nrows = nr < 0 ? 0 : (nr < QF_G ? nr : QF_G);
-        const __amdgpu_buffer_rsrc_t grp = rows_rsrc(q.x + (int64_t)kg * q.ld4 * 4, (uint32_t)nrows * rowbytes);
-        const uint32_t roff = (uint32_t)(k - kg) * rowbytes;
-#pragma unroll
-        for (int j = 0; j < QF_V; ++j) dst[j] = rows_load(grp, voff[j] + roff);
-      } else {
-        const __amdgpu_buffer_rsrc_t rr =
-            rows_rsrc(q.x + (int64_t)k * q.ld4 * 4, k < q.K ? (uint32_t)(q.P4 * 16) : 0u);
-#pragma unroll
-        for (int j = 0; j < QF_V; ++j) dst[j] = rows_load(rr, voff[j]);
-      }
-    };
-#endif
     // one client: g = (L - W)/lr from its loaded row slice t (overwritten with L - W), delta chain and the
     // lane's fp64 sum of squares
     auto client = [&](f4(&t)[QF_V], int kk, float al) -> double {
@@ -668,34 +655,61 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       }
       return acc;
     };
-#if QF_PIPE
-    // software pipeline: client k+1's row slice is requested before client k is computed, so a wave's
-    // loads stay in flight through its ~800 VALU ops per client (two row buffers in registers)
-    // Branch-free: a client k >= K gets an empty range (the loads return zeros and touch no memory), so
-    // the waitcnt pass sees the same loads in flight on every path and never falls back to vmcnt(0).
-    auto issue = [&](f4(&dst)[QF_V], float& al, int k) {
-      // the client's alpha travels with its rows: a load issued later would make the wait for it a
-      // wait for every load in flight (the vector memory counter retires in order)
-      al = q.alpha[k < q.K ? k : q.K - 1];
-      load_rows(dst, k);
+    f4* myrow = rowbuf + (GLDS > 0 ? wave * (NB * QF_V * 64) + lane : 0);
+    const uint32_t ldsbase = (uint32_t)__builtin_amdgcn_readfirstlane(wave) * (NB * QF_V * 64 * 16);
+    // client k's row slice -> this wave's LDS buffer (OOB lanes write 0).  Issued for every client,
+    // k == K included (an empty range: zeros, no memory access), so the wait counts stay the same on
+    // every path and the compiler never falls back to draining the DMA mid-client.
+    auto glds_rows = [&](int k) {
+      const __amdgpu_buffer_rsrc_t rr =
+          rows_rsrc(q.x + (int64_t)k * q.ld4 * 4, k < q.K ? (uint32_t)(q.P4 * 16) : 0u);
+      const uint32_t slot = (uint32_t)(k % NB) * (QF_V * 64 * 16);
+#pragma unroll
+      for (int j = 0; j < QF_V; ++j)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rr, (__attribute__((address_space(3))) void*)(uintptr_t)(ldsbase + slot + (uint32_t)(j * 64 * 16)), 16,
+            voff[j], 0, 0, 2);
     };
-    f4 pb[2][QF_V];
-    float pa[2];
-    issue(pb[0], pa[0], 0);
-#endif
+    // prologue: the first GLDS clients' alphas and slices in flight (alpha before its slice)
+    float al_q[NB];
+    if constexpr (GLDS > 0) {
+#pragma unroll
+      for (int i = 0; i < GLDS; ++i) {
+        al_q[i] = q.alpha[i < q.K ? i : q.K - 1];
+        glds_rows(i);
+      }
+    }
     for (int kg = 0; kg < q.K; kg += QF_G) {
       double v[QF_G];
 #pragma unroll
       for (int jj = 0; jj < QF_G; ++jj) v[jj] = 0.0;
-#if QF_PIPE
-      static_assert(QF_G % 2 == 0, "the two row buffers alternate within a group");
+      if constexpr (GLDS > 0) {
 #pragma unroll
       for (int u = 0; u < QF_G; ++u) {
         const int kk = kg + u;
-        issue(pb[(u + 1) & 1], pa[(u + 1) & 1], kk + 1);  // past K: an empty range (see issue)
-        if (kk < q.K) v[u] = client(pb[u & 1], kk, pa[u & 1]);
+        if (kk >= q.K) break;  // uniform
+        // client kk's slice has landed in LDS: everything issued before the last (GLDS-1) clients'
+        // alpha + 16 slice loads has completed (the vector memory counter retires in order)
+        if constexpr (GLDS == 1)
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else  // (GLDS - 1) x (alpha + 16 slice loads) may stay in flight
+          asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
+        f4 t[QF_V];
+        const f4* src = myrow + (kk % NB) * (QF_V * 64);
+#pragma unroll
+        for (int j = 0; j < QF_V; ++j) t[j] = src[64 * j];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and is in registers: refill the slot
+        const float al = al_q[0];
+#pragma unroll
+        for (int i = 0; i + 1 < NB; ++i) al_q[i] = al_q[i + 1];
+        // the alpha of client kk + GLDS is requested BEFORE its slice, so waiting for it never drains
+        // the DMA; past K: a repeated alpha and an empty range (zeros, no memory access)
+        const int kn = kk + GLDS;
+        al_q[NB - 1] = q.alpha[kn < q.K ? kn : q.K - 1];
+        glds_rows(kn);
+        v[u] = client(t, kk, al);
       }
-#else
+      } else {
       const int nrows = q.K - kg < QF_G ? q.K - kg : QF_G;
       const float* row0 = q.x + (int64_t)kg * q.ld4 * 4;
       const __amdgpu_buffer_rsrc_t grp = rows_rsrc(row0, WIDE ? (uint32_t)nrows * rowbytes : 0u);
@@ -721,7 +735,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
           v[u0 + u] = client(t[u], kk, q.alpha[kk]);
         }
       }
-#endif
+      }
       // multi-reduce: QF_G values per lane -> lane l holds the wave sum of client (l >> s) & (QF_G-1)
       double y;
       const bool b5 = lane & 32, b4 = lane & 16, b3 = lane & 8;
@@ -966,6 +980,20 @@ __global__ __launch_bounds__(256) void k_qfed_gather2b(const double* __restrict_
 }
 static_assert(QF2_ROWS % QF2_SEG == 0, "gather segments must divide the partial rows");
 
+#define QF_GATHER_SEG 16
+__global__ __launch_bounds__(256) void k_qfed_gather_seg(const double* __restrict__ part, int nrows, int K,
+                                                         double* seg) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  const int rps = nrows / QF_GATHER_SEG;
+  const double* p = part + (int64_t)blockIdx.y * rps * K + k;
+  double s = 0.0;
+#pragma unroll 4
+  for (int r = 0; r < rps; ++r) s += p[(int64_t)r * K];
+  seg[(int64_t)blockIdx.y * K + k] = s;
+}
+static_assert(QF_GRID % QF_GATHER_SEG == 0, "gather segments must divide the grid");
+
 __global__ __launch_bounds__(256) void k_qfed_gather(const double* __restrict__ part, int nblk, int K,
                                                      double* sqnorm) {
   const int k = blockIdx.x * 256 + threadIdx.x;
@@ -978,12 +1006,18 @@ __global__ __launch_bounds__(256) void k_qfed_gather(const double* __restrict__ 
 extern "C" int fa_qfed_max_chunk(void) { return QF_MAXK; }
 extern "C" int64_t fa_qfed_workspace_bytes(int32_t K) {  // enough for either kernel family
   const int64_t k = K > 0 ? K : 1;
-  const int64_t w1 = (int64_t)QF_GRID * k * 8, w2 = ((int64_t)QF2_ROWS + QF2_SEG) * k * 8;
+  const int64_t w1 = ((int64_t)QF_GRID + QF_GATHER_SEG) * k * 8, w2 = ((int64_t)QF2_ROWS + QF2_SEG) * k * 8;
   return w1 > w2 ? w1 : w2;
 }
 
 #ifndef QF_CHAIN_KERNEL
 #define QF_CHAIN_KERNEL 1
+#endif
+#ifndef QF_CHAIN_GLDS
+#define QF_CHAIN_GLDS 1  // LDS-DMA slices per wave of the chain launches (profiles/r02_tune_qfed2.log)
+#endif
+#ifndef QF_PLAIN_GLDS
+#define QF_PLAIN_GLDS 0
 #endif
 
 static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const float* last, const float* alpha,
@@ -1010,18 +1044,23 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
       if (qw.sw < 1) qw.sw = 1;
       if (qw.sw > QF_V || !QF_BALANCE) qw.sw = QF_V;
     }
+    // chain launches: LDS-DMA prefetch (QF_CHAIN_GLDS slices); the plain kernel: register loads
     if (wide && chain)
-      hipLaunchKernelGGL((k_qfed_accum<true, true>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<true, true, QF_CHAIN_GLDS>), dim3(QF_GRID), dim3(256), 0, st, qw);
     else if (wide)
-      hipLaunchKernelGGL((k_qfed_accum<true, false>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<true, false, QF_PLAIN_GLDS>), dim3(QF_GRID), dim3(256), 0, st, qw);
     else if (chain)
-      hipLaunchKernelGGL((k_qfed_accum<false, true>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<false, true, QF_CHAIN_GLDS>), dim3(QF_GRID), dim3(256), 0, st, qw);
     else
-      hipLaunchKernelGGL((k_qfed_accum<false, false>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<false, false, QF_PLAIN_GLDS>), dim3(QF_GRID), dim3(256), 0, st, qw);
     int e = check_launch("fa_qfed_accumulate");
     if (e) return e;
-    hipLaunchKernelGGL(k_qfed_gather, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)workspace,
-                       (int)QF_GRID, (int)K, sqnorm);
+    // the QF_GRID partial rows, summed in a fixed two-level order (16 segments of QF_GRID/16 rows)
+    double* seg = (double*)workspace + (int64_t)QF_GRID * K;
+    hipLaunchKernelGGL(k_qfed_gather_seg, dim3((K + 255) / 256, QF_GATHER_SEG), dim3(256), 0, st,
+                       (const double*)workspace, (int)QF_GRID, (int)K, seg);
+    hipLaunchKernelGGL(k_qfed_gather, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)seg,
+                       (int)QF_GATHER_SEG, (int)K, sqnorm);
     e = check_launch("fa_qfed_accumulate(gather)");
     if (e) return e;
     if (pw >= P - w0) break;

@@ -622,3 +622,39 @@ def test_heterofl_int64_entries_follow_the_reference_cast(gpu_device):
     combine_prefix_boxes(got, locs, device=gpu_device)
     for n in glob:
         assert got[n].dtype == want[n].dtype and torch.equal(got[n], want[n]), n
+
+
+@pytest.mark.parametrize("K,P", [(1, 5), (3, 1000), (7, 70001), (64, 1_000_003), (13, 4_194_307)])
+def test_qfed_fused_chain_kernel(gpu_device, K, P):
+    """fa_qfed_accumulate with the fused FedAvg chain (LDS-DMA prefetch kernel): delta and the norms equal the
+    plain launch's bit for bit, the chain equals fa_reduce's FedAvg sum of the same rows bit for bit, and a
+    chunked launch pair continues both chains exactly (FA_ACCUMULATE)."""
+    from fedscale_amd import kernels as kx
+    from fedscale_amd import synth
+    from fedscale_amd.bucket import round_up
+
+    ld = round_up(P, 64)
+    x = torch.empty(K, ld, device="cuda")
+    synth.fill(x, K, P, seed=K + P)
+    last = torch.empty(1, ld, device="cuda")
+    synth.fill(last, 1, P, seed=K + P + 90000, scale_noise=0.0)
+    last = last[0]
+    alpha = torch.rand(K, device="cuda") + 0.5
+    ws = kx.qfed_workspace(K, "cuda")
+    outs = {}
+    for use_chain in (False, True):
+        delta = torch.full((ld,), float("nan"), device="cuda")
+        chain = torch.full((ld,), float("nan"), device="cuda") if use_chain else None
+        sq = torch.zeros(K, dtype=torch.float64, device="cuda")
+        h = max(1, K // 2)
+        kx.qfed_accumulate(x[:h], h, P, last=last, alpha=alpha[:h], lr=0.05, delta=delta, sqnorm=sq[:h],
+                           workspace=ws, accumulate=False, chain=chain)
+        if K > h:
+            kx.qfed_accumulate(x[h:], K - h, P, last=last, alpha=alpha[h:], lr=0.05, delta=delta, sqnorm=sq[h:],
+                               workspace=ws, accumulate=True, chain=chain)
+        outs[use_chain] = (delta[:P].clone(), sq.clone(), None if chain is None else chain[:P].clone())
+    assert torch.equal(outs[True][0], outs[False][0])
+    assert torch.equal(outs[True][1], outs[False][1])
+    want = torch.empty(ld, device="cuda")
+    kx.reduce(x, K, P, want)
+    assert torch.equal(outs[True][2], want[:P])
