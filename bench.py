@@ -79,6 +79,9 @@ def parse():
                                                                      "every CPU leg)")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--no-other-configs", action="store_true", help="skip the side measurements (other_configs)")
+    ap.add_argument("--mem-fraction", type=float, default=0.6,
+                    help="share of the free HBM a workload's resident client chunk may take (lower it when several "
+                         "ranks share one GPU in a rehearsal)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse ranks sharing a GPU")
     a = ap.parse_args()
@@ -447,8 +450,12 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend):
     return _max_over_ranks([wall, kern_ms], dev, world, backend), kern_ms
 
 
+MEM_FRACTION = 0.6
+
+
 def config_line(name, cfg, dev, rank, world, shards, seed, backend, steps=5, warmup=2, **kw) -> dict:
     """A BASELINE config on all ranks (parameter-sharded over them), for other_configs."""
+    kw.setdefault("budget_fraction", MEM_FRACTION)
     w = Workload(cfg["policy"], cfg["clients"], cfg["params"], rank, world, dev, seed, shards, **kw)
     (wall, kern_max), _ = time_workload(w, steps, warmup, dev, world, backend)
     ms = wall * 1e3 / steps
@@ -516,7 +523,9 @@ def main():
     cfg = args.cfg
     policy, K, P = cfg["policy"], cfg["clients"], cfg["params"]
     weak = args.scaling == "weak"
-    w = Workload(policy, K, P, rank, world, dev, args.seed, shards, weak=weak)
+    global MEM_FRACTION
+    MEM_FRACTION = args.mem_fraction
+    w = Workload(policy, K, P, rank, world, dev, args.seed, shards, weak=weak, budget_fraction=args.mem_fraction)
     (wall, kern_ms_max), kern_ms = time_workload(w, args.steps, args.warmup, dev, world, args.dist_backend)
     strong = not weak and not w.cmode
 

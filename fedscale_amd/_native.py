@@ -20,6 +20,7 @@ FA_YOGI_INIT = 4
 FA_DP_WRITE_PARAM = 1
 FA_DP_SCALE_ONLY = 2
 FA_DT_F32, FA_DT_F64, FA_DT_I64 = 0, 1, 2
+FA_SGD_NESTEROV, FA_SGD_FIRST = 1, 2
 
 
 class FedAggError(RuntimeError):
@@ -70,6 +71,8 @@ SIGNATURES = {
     "fa_prox_update": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _f32, _c_void_p]),
     "fa_sgd_prox_step": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _f32, _f32, _f64,
                                 _f32, _i32, _i32, _f32, _i32, _c_void_p]),
+    "fa_sgd_prox_step_groups": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p,
+                                       _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32, _i32, _c_void_p]),
     "fa_dp_workspace_bytes": (_i64, [_c_void_p, _i32]),
     "fa_dp_clip_coef": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _f32, _i32, _c_void_p, _c_void_p,
                                _c_void_p]),

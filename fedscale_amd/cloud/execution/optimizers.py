@@ -9,7 +9,7 @@ reference's fp32 arithmetic:
     param.data += conf.learning_rate * conf.proxy_mu * (param.data - global_model[idx])
 
 ``step_and_update(optimizer, conf, model, global_model)`` fuses the executor's preceding
-``torch.optim.SGD.step()`` (torch_client.py:236) into the same pass (``fa_sgd_prox_step``).
+``torch.optim.SGD.step()`` (torch_client.py:236) into the same pass (``fa_sgd_prox_step_groups``).
 
 The parameters and ``global_model`` must live on the GPU (an executor training on the MI355X); there is
 no CPU fallback.  Any ``gradient_policy`` other than ``'fed-prox'`` is a no-op, as in the reference.
@@ -17,6 +17,7 @@ no CPU fallback.  Any ``gradient_policy`` other than ``'fed-prox'`` is a no-op, 
 from __future__ import annotations
 
 from ... import kernels as kx
+from ..._native import FA_SGD_FIRST as kx_first, FA_SGD_NESTEROV as kx_nesterov
 
 
 class ClientOptimizer(object):
@@ -69,9 +70,9 @@ class ClientOptimizer(object):
 
     def step_and_update(self, optimizer, conf, model, global_model=None, fma=True):
         """torch_client.py:236-240, ``optimizer.step()`` then ``update_client_weight(conf, model,
-        global_model)``, as one multi-tensor launch per parameter group (``fa_sgd_prox_step``): one pass
-        over param, grad, momentum buffer and global model instead of torch's SGD passes plus the proximal
-        pass. ``optimizer`` is the ``torch.optim.SGD`` of get_optimizer (torch_client.py:95-130); its
+        global_model)``, as ONE multi-tensor launch over every parameter group (``fa_sgd_prox_step_groups``,
+        the groups' lr / momentum / dampening / weight decay per tensor): one pass over param, grad,
+        momentum buffer and global model instead of torch's SGD passes plus the proximal pass. ``optimizer`` is the ``torch.optim.SGD`` of get_optimizer (torch_client.py:95-130); its
         momentum buffers stay in ``optimizer.state``, so it can still be stepped directly. Any other
         optimizer (Adam for 'nlp', maximize / differentiable SGD) takes the two reference calls."""
         import torch
@@ -85,30 +86,34 @@ class ClientOptimizer(object):
             optimizer.step()
             return self.update_client_weight(conf, model, global_model)
         c = float(conf.learning_rate * conf.proxy_mu) if prox else 0.0
-        stepped = set()
+        # every param group in ONE launch: per-tensor lr / momentum / dampening / weight decay / flags, as
+        # torch.optim.SGD keeps them per group (the detection task makes one group per parameter)
+        ps, grads, bufs, fresh, lr, mom, damp, wd, flags = [], [], [], [], [], [], [], [], []
         for group in optimizer.param_groups:
-            mom = float(group['momentum'])
-            ps = [p for p in group['params'] if p.grad is not None]
-            parts = {True: [], False: []}  # first step of the momentum buffer / later steps
-            for p in ps:
-                st = optimizer.state[p]
-                parts[mom != 0 and st.get('momentum_buffer') is None].append(p)
-            for first, part in parts.items():
-                if not part:
+            m = float(group['momentum'])
+            nest = kx_nesterov if group['nesterov'] else 0
+            for p in group['params']:
+                if p.grad is None:
                     continue
-                bufs = None
-                if mom != 0:
-                    # new buffers enter optimizer.state only once the launch has been accepted: a call
-                    # that raises must not leave uninitialised momentum behind for the next step
-                    bufs = ([torch.empty_like(p, memory_format=torch.contiguous_format) for p in part] if first
-                            else [optimizer.state[p]['momentum_buffer'] for p in part])
-                kx.sgd_prox_step(part, [p.grad for p in part], bufs, [gmap[id(p)] for p in part] if prox else None,
-                                 group['lr'], mom, group['dampening'], group['weight_decay'], group['nesterov'],
-                                 first, c, fma=fma)
-                if mom != 0 and first:
-                    for p, b in zip(part, bufs):
-                        optimizer.state[p]['momentum_buffer'] = b
-                stepped.update(id(p) for p in part)
+                buf = optimizer.state[p].get('momentum_buffer') if m != 0 else None
+                first = m != 0 and buf is None
+                if first:  # enters optimizer.state only once the launch has been accepted (below)
+                    buf = torch.empty_like(p, memory_format=torch.contiguous_format)
+                    fresh.append((p, buf))
+                ps.append(p)
+                grads.append(p.grad)
+                bufs.append(buf)
+                lr.append(group['lr'])
+                mom.append(m)
+                damp.append(group['dampening'])
+                wd.append(group['weight_decay'])
+                flags.append(nest | (kx_first if first else 0))
+        if ps:
+            kx.sgd_prox_step_groups(ps, grads, bufs, [gmap[id(p)] for p in ps] if prox else None, lr, mom, damp,
+                                    wd, flags, c, fma=fma)
+        for p, buf in fresh:
+            optimizer.state[p]['momentum_buffer'] = buf
+        stepped = {id(p) for p in ps}
         if prox:  # parameters without a gradient still take the proximal step (optimizers.py:8-10)
             rest = [(p, global_model[i]) for i, p in enumerate(params) if id(p) not in stepped]
             if rest:

@@ -164,7 +164,7 @@ class ShardedModelAdapter(TorchModelAdapter):
     def _copy_to_host(self, f_cpu: torch.Tensor, s_cpu: torch.Tensor):
         """Per-part D2H into the pinned snapshot (each over its own device's link); no collective."""
         for p in self.parts:
-            p._ready.synchronize()
+            p._ready.synchronize()  # every part's round, whatever stream it ran on
         for p in self.parts:
             L = p.layout
             if L.P:

@@ -132,6 +132,7 @@ class TorchModelAdapter(ModelAdapterBase):
         self._f[0].copy_(cur_f)
         self._s[0].copy_(cur_s.to(torch.int64))
         self._ready = torch.cuda.Event()  # the kernels that wrote the current model buffers
+        self._ready_stream = torch.cuda.current_stream(self.device)
         self._init_egress(_load_from is None)
 
     def _init_egress(self, module_in_sync: bool):
@@ -155,7 +156,8 @@ class TorchModelAdapter(ModelAdapterBase):
         return self._f[1 - self._cur], self._s[1 - self._cur]
 
     def _commit_scratch(self):
-        self._ready.record(torch.cuda.current_stream(self.device))
+        self._ready_stream = torch.cuda.current_stream(self.device)
+        self._ready.record(self._ready_stream)
         with self._egress_lock:  # (buffer, version) flip atomically for the servicer threads
             self._cur = 1 - self._cur
             self._version += 1
@@ -204,10 +206,12 @@ class TorchModelAdapter(ModelAdapterBase):
         lock, so no round commits meanwhile; synchronous).  Parameter-sharded SPMD ranks all-gather
         first: every rank must then call egress from its main thread, in step (bench / tests)."""
         L = self.layout
-        self._ready.synchronize()
+        if torch.cuda.current_stream(self.device) != self._ready_stream:
+            self._ready.synchronize()  # another stream wrote the model: the blocking copy alone would not wait
         full = self.shards.all_gather(self._f[self._cur])
         f_cpu[:L.P_full].copy_(full[:L.P_full])
-        s_cpu[:L.Q].copy_(self._s[self._cur][:L.Q])
+        if L.Q:
+            s_cpu[:L.Q].copy_(self._s[self._cur][:L.Q])
 
     def _acquire_host(self) -> "_HostSnapshot":
         """The host snapshot of the current model version (one D2H per version), held by the caller until
@@ -333,7 +337,12 @@ class TorchModelAdapter(ModelAdapterBase):
         if self.shards.shards_clients:  # this rank stages only its block of the arrivals
             k0, k1 = self.shards.client_block(K)
             K_local = max(1, k1 - k0)
-        want = min(cap or default_capacity(self.layout, K_local, self.device), K_local)
+        if cap:
+            want = min(cap, K_local)
+        elif self.staging is not None and self.staging.capacity >= K_local:
+            want = K_local  # the round fits the staging already allocated (no free-memory query)
+        else:
+            want = min(default_capacity(self.layout, K_local, self.device), K_local)
         if policy == "qfedavg":  # phase-1 chunks hold at most fa_qfed_max_chunk() clients
             want = min(want, kx_qfed_max_chunk())
         if self.staging is None or self.staging.capacity < want:

@@ -145,18 +145,24 @@ __global__ __launch_bounds__(MT_THREADS) void k_prox(MtList L, float c) {
 // plus the proximal pass.  `fma`: torch's alpha-adds (add(x, alpha=a), mul_().add_()) as one fused
 // multiply-add each, the way its elementwise kernels are contracted on ROCm; 0: every op rounded.
 // ------------------------------------------------------------------------------------------------
+constexpr int SGD_MAX = 48;  // tensors per SGD launch: pointers + per-tensor scalars stay < 3 KiB of arguments
 struct SgdList {
-  float* p[MT_MAX];
-  const float* g[MT_MAX];      // gradient
-  float* m[MT_MAX];            // momentum buffer (NULL when momentum == 0)
-  const float* w[MT_MAX];      // global model (NULL: no proximal step)
-  int64_t n[MT_MAX];
-  int32_t blk0[MT_MAX + 1];
+  float* p[SGD_MAX];
+  const float* g[SGD_MAX];      // gradient
+  float* m[SGD_MAX];            // momentum buffer (NULL when the tensor's momentum == 0)
+  const float* w[SGD_MAX];      // global model (NULL: no proximal step)
+  int64_t n[SGD_MAX];
+  // per tensor, from its param group (torch_client.py:100-108 builds one group per parameter for
+  // detection): lr, momentum, fp32(1 - dampening) formed in double as torch does, weight decay, flags
+  float lr[SGD_MAX], mom[SGD_MAX], omd[SGD_MAX], wd[SGD_MAX];
+  uint8_t flags[SGD_MAX];       // SGD_NESTEROV | SGD_FIRST
+  int32_t blk0[SGD_MAX + 1];
   uint64_t vec;
   int32_t T;
 };
+enum { SGD_NESTEROV = 1, SGD_FIRST = 2 };
 struct SgdScalars {
-  float lr, momentum, omd, wd, c;  // omd = fp32(1 - dampening), computed in double as torch does
+  float lr, momentum, omd, wd, c;
   int32_t nesterov, first, fma, prox;
 };
 __device__ __forceinline__ float axpy(float a, float x, float y, int fma) {  // y + a * x
@@ -172,7 +178,7 @@ __device__ __forceinline__ void sgd1(float& p, float g, float& m, float w, const
   p = axpy(-k.lr, d, p, k.fma);                                 // param.add_(d, alpha=-lr)
   if (k.prox) p = p + k.c * (p - w);                            // optimizers.py:10 (separate torch ops)
 }
-__global__ __launch_bounds__(MT_THREADS) void k_sgd_prox(SgdList L, SgdScalars k) {
+__global__ __launch_bounds__(MT_THREADS) void k_sgd_prox(SgdList L, float c, int fma) {
   int lo = 0, hi = L.T - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -185,6 +191,8 @@ __global__ __launch_bounds__(MT_THREADS) void k_sgd_prox(SgdList L, SgdScalars k
   const float* __restrict__ g = L.g[t];
   float* __restrict__ m = L.m[t];
   const float* __restrict__ w = L.w[t];
+  const SgdScalars k{L.lr[t], L.mom[t], L.omd[t], L.wd[t], c, (L.flags[t] & SGD_NESTEROV) ? 1 : 0,
+                     (L.flags[t] & SGD_FIRST) ? 1 : 0, fma, w ? 1 : 0};
   const bool hasm = k.momentum != 0.f;
   if ((L.vec >> t) & 1) {
 #pragma unroll
@@ -460,51 +468,90 @@ extern "C" int fa_prox_update(float* const* param, const float* const* global, c
   return FA_OK;
 }
 
-extern "C" int fa_sgd_prox_step(float* const* param, const float* const* grad, float* const* momentum_buf,
-                                const float* const* global, const int64_t* numel, int32_t T, float lr,
-                                float momentum, double dampening, float weight_decay, int32_t nesterov,
-                                int32_t first, float c, int32_t fma, fa_stream_t stream) {
-  int rc = check_list("fa_sgd_prox_step", T, param, grad, numel, true);
+static int sgd_groups(const char* what, float* const* param, const float* const* grad,
+                      float* const* momentum_buf, const float* const* global, const int64_t* numel, int32_t T,
+                      const float* lr, const float* momentum, const double* dampening, const float* weight_decay,
+                      const int32_t* flags, float c, int32_t fma, fa_stream_t stream) {
+  int rc = check_list(what, T, param, grad, numel, true);
   if (rc) return rc;
+  if (T > 0 && (!lr || !momentum || !dampening || !weight_decay || !flags))
+    return fail(FA_E_ARG, "%s: NULL per-tensor scalar table", what);
   for (int i = 0; i < T; ++i) {
     if (numel[i] == 0) continue;
-    if (momentum != 0.f && (!momentum_buf || !momentum_buf[i]))
-      return fail(FA_E_ARG, "fa_sgd_prox_step: tensor %d: momentum != 0 needs a momentum buffer", i);
-    if (global && !global[i]) return fail(FA_E_ARG, "fa_sgd_prox_step: tensor %d: NULL global pointer", i);
+    if (momentum[i] != 0.f && (!momentum_buf || !momentum_buf[i]))
+      return fail(FA_E_ARG, "%s: tensor %d: momentum != 0 needs a momentum buffer", what, i);
+    if (global && !global[i]) return fail(FA_E_ARG, "%s: tensor %d: NULL global pointer", what, i);
     if ((momentum_buf && ((uintptr_t)momentum_buf[i] & 3u)) || (global && ((uintptr_t)global[i] & 3u)))
-      return fail(FA_E_ARG, "fa_sgd_prox_step: tensor %d: pointers must be 4-byte aligned", i);
+      return fail(FA_E_ARG, "%s: tensor %d: pointers must be 4-byte aligned", what, i);
+    if ((flags[i] & SGD_NESTEROV) && (momentum[i] <= 0.f || dampening[i] != 0.0))
+      return fail(FA_E_ARG, "%s: tensor %d: nesterov needs momentum > 0 and zero dampening", what, i);
   }
-  if (nesterov && (momentum <= 0.f || dampening != 0.0))
-    return fail(FA_E_ARG, "fa_sgd_prox_step: nesterov needs momentum > 0 and zero dampening");
-  // torch's buf.add_(d, alpha=1 - dampening): the Python double 1 - dampening, rounded to fp32 once
-  SgdScalars k{lr, momentum, (float)(1.0 - dampening), weight_decay, c, nesterov ? 1 : 0, first ? 1 : 0, fma ? 1 : 0,
-               global ? 1 : 0};
   int32_t t = 0;
   while (t < T) {
     SgdList L;
     L.T = 0;
     L.vec = 0;
     int32_t blk = 0;
-    while (t < T && L.T < MT_MAX) {
+    while (t < T && L.T < SGD_MAX) {
       const int64_t nb = (numel[t] + MT_CHUNK - 1) / MT_CHUNK;
       if (L.T > 0 && blk + nb > (int64_t)INT32_MAX / 2) break;
-      L.p[L.T] = param[t];
-      L.g[L.T] = grad[t];
-      L.m[L.T] = (momentum != 0.f) ? momentum_buf[t] : nullptr;
-      L.w[L.T] = global ? global[t] : nullptr;
-      L.n[L.T] = numel[t];
-      L.blk0[L.T] = blk;
-      if (al16(L.p[L.T]) && al16(L.g[L.T]) && al16(L.m[L.T]) && al16(L.w[L.T])) L.vec |= (uint64_t)1 << L.T;
+      const int j = L.T;
+      L.p[j] = param[t];
+      L.g[j] = grad[t];
+      L.m[j] = (momentum[t] != 0.f) ? momentum_buf[t] : nullptr;
+      L.w[j] = global ? global[t] : nullptr;
+      L.n[j] = numel[t];
+      L.lr[j] = lr[t];
+      L.mom[j] = momentum[t];
+      // torch's buf.add_(d, alpha=1 - dampening): the Python double 1 - dampening, rounded to fp32 once
+      L.omd[j] = (float)(1.0 - dampening[t]);
+      L.wd[j] = weight_decay[t];
+      L.flags[j] = (uint8_t)(flags[t] & (SGD_NESTEROV | SGD_FIRST));
+      L.blk0[j] = blk;
+      if (al16(L.p[j]) && al16(L.g[j]) && al16(L.m[j]) && al16(L.w[j])) L.vec |= (uint64_t)1 << j;
       blk += (int32_t)nb;
       ++L.T;
       ++t;
     }
     L.blk0[L.T] = blk;
     if (blk == 0) continue;
-    hipLaunchKernelGGL(k_sgd_prox, dim3(blk), dim3(MT_THREADS), 0, (hipStream_t)stream, L, k);
-    if ((rc = check_launch("fa_sgd_prox_step"))) return rc;
+    hipLaunchKernelGGL(k_sgd_prox, dim3(blk), dim3(MT_THREADS), 0, (hipStream_t)stream, L, c, fma ? 1 : 0);
+    if ((rc = check_launch(what))) return rc;
   }
   return FA_OK;
+}
+
+extern "C" int fa_sgd_prox_step(float* const* param, const float* const* grad, float* const* momentum_buf,
+                                const float* const* global, const int64_t* numel, int32_t T, float lr,
+                                float momentum, double dampening, float weight_decay, int32_t nesterov,
+                                int32_t first, float c, int32_t fma, fa_stream_t stream) {
+  if (T < 0) return fail(FA_E_ARG, "fa_sgd_prox_step: T=%d", (int)T);
+  if (nesterov && (momentum <= 0.f || dampening != 0.0))
+    return fail(FA_E_ARG, "fa_sgd_prox_step: nesterov needs momentum > 0 and zero dampening");
+  // one group: every tensor takes the same scalars
+  const int32_t f = (nesterov ? SGD_NESTEROV : 0) | (first ? SGD_FIRST : 0);
+  int rc = FA_OK;
+  for (int32_t t0 = 0; t0 < T && rc == FA_OK; t0 += SGD_MAX) {
+    const int32_t n = T - t0 < SGD_MAX ? T - t0 : SGD_MAX;
+    float lrs[SGD_MAX], moms[SGD_MAX], wds[SGD_MAX];
+    double damps[SGD_MAX];
+    int32_t flags[SGD_MAX];
+    for (int i = 0; i < n; ++i) {
+      lrs[i] = lr; moms[i] = momentum; wds[i] = weight_decay; damps[i] = dampening; flags[i] = f;
+    }
+    rc = sgd_groups("fa_sgd_prox_step", param + t0, grad + t0, momentum_buf ? momentum_buf + t0 : nullptr,
+                    global ? global + t0 : nullptr, numel + t0, n, lrs, moms, damps, wds, flags, c, fma, stream);
+  }
+  if (T == 0) rc = check_list("fa_sgd_prox_step", T, param, grad, numel, true);
+  return rc;
+}
+
+extern "C" int fa_sgd_prox_step_groups(float* const* param, const float* const* grad, float* const* momentum_buf,
+                                       const float* const* global, const int64_t* numel, int32_t T, const float* lr,
+                                       const float* momentum, const double* dampening, const float* weight_decay,
+                                       const int32_t* flags, float c, int32_t fma, fa_stream_t stream) {
+  return sgd_groups("fa_sgd_prox_step_groups", param, grad, momentum_buf, global, numel, T, lr, momentum,
+                    dampening, weight_decay, flags, c, fma, stream);
 }
 
 extern "C" int64_t fa_dp_workspace_bytes(const int64_t* numel, int32_t T) {

@@ -313,6 +313,50 @@ def sgd_prox_step(params, grads, bufs, global_model, lr: float, momentum: float,
          int(bool(fma)), _stream(params[0]))
 
 
+def sgd_prox_step_groups(params, grads, bufs, global_model, lr, momentum, dampening, weight_decay, flags,
+                         c: float, fma: bool = True):
+    """torch.optim.SGD step (per-tensor group scalars) + FedProx over every tensor in one multi-tensor
+    launch (fa_sgd_prox_step_groups).  ``bufs[i]`` None where the tensor's momentum is 0; ``global_model``
+    None: no proximal step; scalars are sequences of len(params); flags: FA_SGD_NESTEROV | FA_SGD_FIRST."""
+    import numpy as np
+
+    params, grads = list(params), list(grads)
+    T = len(params)
+    if not T:
+        return
+    bufs = list(bufs) if bufs is not None else [None] * T
+    global_model = list(global_model) if global_model is not None else None
+
+    def build():
+        dev = _fp32_list(params, "param")
+        for name, lst, none_ok in (("grad", grads, False), ("momentum_buffer", bufs, True),
+                                   ("global_model", global_model, False)):
+            if lst is None:
+                continue
+            if len(lst) != T:
+                raise ValueError(f"{T} parameters but {len(lst)} {name} tensors")
+            _fp32_list(lst, name, dev, allow_none=none_ok)
+            for i, (p, t) in enumerate(zip(params, lst)):
+                if t is not None and p.shape != t.shape:
+                    raise ValueError(f"{name}[{i}] shape {tuple(t.shape)} != param[{i}] shape {tuple(p.shape)}")
+        return _Plan([params, grads, bufs, global_model if global_model is not None else [None] * T],
+                     [p.numel() for p in params])
+
+    plan = _cached_plan("sgdgroups", (params, grads, bufs, global_model), build)
+    lr_a = np.asarray(lr, dtype=np.float32)
+    mom_a = np.asarray(momentum, dtype=np.float32)
+    damp_a = np.asarray(dampening, dtype=np.float64)
+    wd_a = np.asarray(weight_decay, dtype=np.float32)
+    fl_a = np.asarray(flags, dtype=np.int32)
+    for a in (lr_a, mom_a, damp_a, wd_a, fl_a):
+        if a.shape != (T,):
+            raise ValueError(f"per-tensor scalars: expected {T} values, got shape {a.shape}")
+    call("fa_sgd_prox_step_groups", plan.ptr(0), plan.ptr(1), plan.ptr(2),
+         plan.ptr(3) if global_model is not None else None, plan.numel.ctypes.data, T, lr_a.ctypes.data,
+         mom_a.ctypes.data, damp_a.ctypes.data, wd_a.ctypes.data, fl_a.ctypes.data, float(c), int(bool(fma)),
+         _stream(params[0]))
+
+
 def dp_clip_coef(params, last, max_norm: float, norm_inf: bool, coef_out: torch.Tensor):
     """coef_out[0:3] <- (total norm of param - last, clip coefficient, apply flag) (fa_dp_clip_coef)."""
     params = list(params)

@@ -75,8 +75,11 @@ class DeviceRound:
         self.chunks_done = 0
         dev, L = self.device, layout
         self.acc = None  # running fp32 chain across chunks
-        self.acc_i = torch.zeros(L.ldq, dtype=torch.int64, device=dev)
-        self.acc_d = torch.zeros(L.ldq, dtype=torch.float64, device=dev)
+        # int64 / float64 side sums: the first chunk's accumulate overwrites them, so no memset is needed
+        # unless a client-mode rank may contribute nothing to the cross-rank sum
+        alloc = torch.zeros if self.cg is not None else torch.empty
+        self.acc_i = alloc(L.ldq, dtype=torch.int64, device=dev)
+        self.acc_d = alloc(L.ldq, dtype=torch.float64, device=dev)
         self._w32 = np.zeros(self.cap, dtype=np.float32)  # per-slot weights of the current chunk
         self._w64 = np.zeros(self.cap, dtype=np.float64)
         self.last_f32, self.last_i64 = last_f32, last_i64

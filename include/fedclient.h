@@ -55,6 +55,19 @@ int fa_sgd_prox_step(float* const* param, const float* const* grad, float* const
                      fa_stream_t stream);
 
 /*
+ * fa_sgd_prox_step over every param group of an optimizer in one pass: the SGD scalars come per tensor
+ * (host arrays of T: lr, momentum, dampening (the group's Python double), weight_decay, flags =
+ * FA_SGD_NESTEROV | FA_SGD_FIRST), as torch.optim.SGD keeps them per param group.  The detection task
+ * builds one group per parameter (torch_client.py:100-108), so this is one launch where the per-group
+ * call would be one launch (and one host round trip) per parameter.
+ */
+enum { FA_SGD_NESTEROV = 1, FA_SGD_FIRST = 2 };
+int fa_sgd_prox_step_groups(float* const* param, const float* const* grad, float* const* momentum_buf,
+                            const float* const* global, const int64_t* numel, int32_t T, const float* lr,
+                            const float* momentum, const double* dampening, const float* weight_decay,
+                            const int32_t* flags, float c, int32_t fma, fa_stream_t stream);
+
+/*
  * Local-DP clipping coefficient, examples/differential_privacy/clip_norm.py:12-52 applied to
  * delta[t] = param[t] - last[t] (customized_client.py:51-55; last[t] == NULL: delta[t] = param[t]):
  *   norms[t] = ||delta[t]||_2 (fp32)  ->  total = ||stack(norms)||_2   (norm_inf: max |delta|)
