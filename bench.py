@@ -377,7 +377,7 @@ class Workload:
                 self.shards.all_reduce_sum(qf["delta"])
                 self.shards.all_reduce_sum(qf["sq"])
             elif self.world > 1:  # the one exchange of parameter sharding: per-client norms over the shards
-                self.shards.all_reduce_sum(qf["sq"])
+                self.shards.sum_partials(qf["sq"])
             kx.qfed_hs(qf["sq"], qf["c1"], qf["c2"], self.Kg, qf["hs"])
             kx.qfed_finalize(qf["last"], qf["delta"], qf["hs"], self.out, P)
             return

@@ -163,7 +163,7 @@ class TorchModelAdapter(ModelAdapterBase):
             self._version += 1
 
     def _sqnorm_allreduce(self):
-        return self.shards.all_reduce_sum if self.shards.shards_params else None
+        return self.shards.sum_partials if self.shards.shards_params else None
 
     def _pack_values(self, values: list, f_dst: torch.Tensor, s_dst: torch.Tensor):
         """weights list -> device fp32 bucket slice + side table (converted to s_dst's dtype)."""

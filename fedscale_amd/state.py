@@ -4,13 +4,16 @@
 ``f32`` is this rank's slice of the fp32 bucket, ``side`` the replicated side table (int64 for a model
 state, float64 for a FedAvg mean of int64 entries).
 
-Two ways to spread a round over the GPUs of a node (one process per GPU, torch.distributed over RCCL;
-SURVEY §8e):
+``DeviceGroup`` is the N GPUs that ONE process drives: the multi-GPU drop-in behind FedScale's single
+aggregator process (``ShardedModelAdapter``; its cross-device steps are RCCL collectives issued from the
+library, ``fa_rccl_*``).  ``ShardGroup`` is one process per GPU, torch.distributed over RCCL (the SPMD
+benchmark and tests), with two ways to spread a round over the ranks:
 
 * ``mode="params"`` (default): every rank owns an equal-size slice of the fp32 bucket and reduces its
   slice of every client update.  The only collectives are the all-gather that reassembles the global model
-  for egress and, for q-FedAvg, one all-reduce of the K per-client squared norms.  The per-element chain
-  is the reference's, so the result is bit-exact.
+  for egress and, for q-FedAvg, one exchange of the K per-client partial squared norms (all-gather +
+  fixed-order sum, ``sum_partials``).  The per-element chain is the reference's, so the result is
+  bit-exact.
 * ``mode="clients"``: every rank holds the whole model and reduces a contiguous block of the round's
   arrivals (rank r takes arrival indices [r*K/N, (r+1)*K/N)).  The per-rank partial sums meet in one RCCL
   all-reduce (the "final RCCL reduce" of the north star) and the server step then runs replicated, so
@@ -91,6 +94,24 @@ class ShardGroup:
             return t
         return self.collective_all_reduce(t)
 
+    def sum_partials(self, t: torch.Tensor) -> torch.Tensor:
+        """In-place sum over ranks in a FIXED rank order (all-gather, then ((t_0 + t_1) + t_2) + ...): the
+        per-client partial squared norms of q-FedAvg over the parameter shards.  Unlike an all-reduce,
+        whose internal order depends on the ring, the bits do not depend on the transport."""
+        if self.world == 1:
+            return t
+        allp = self.collective_all_gather(t.reshape(-1)).view(self.world, -1)
+        if t.device.type == "cuda" and t.dtype == torch.float64:
+            from . import kernels as kx
+
+            kx.sum_rows_f64(allp, t.view(-1))
+            return t
+        acc = allp[0].clone()
+        for r in range(1, self.world):
+            acc += allp[r]
+        t.copy_(acc.view_as(t))
+        return t
+
     # raw collectives (no world-1 short cut): what the wrappers above issue, callable at any world size
     def collective_all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         import torch.distributed as dist
@@ -131,6 +152,9 @@ class PartOf(ShardGroup):
         raise RuntimeError("in-process shard: the coordinating adapter reassembles the parts")
 
     def all_reduce_sum(self, t):
+        raise RuntimeError("in-process shard: the coordinating adapter combines the parts")
+
+    def sum_partials(self, t):
         raise RuntimeError("in-process shard: the coordinating adapter combines the parts")
 
 
