@@ -504,11 +504,13 @@ struct QfArgs {
 // the client must have |a| in [2^-80, 2^80) or a == 0 (NaN propagates correctly either way); otherwise
 // (a denormal, huge or infinite element anywhere in the wave) the wave redoes that client with the
 // IEEE division.  The range test is folded per lane into min/max of frexp exponents + max |a|, one wave
-// vote per client.
+// vote per client.  The residual is formed negated, nrem = b*q - a, and the correction is q - nrem*r:
+// the same exact values for a != 0, and the signed zero IEEE gives for a = -0 (b > 0: q = -0,
+// nrem = +0, -0 + -0 = -0), where q + (a - b*q)*r would round -0 + +0 to +0.
 __device__ __forceinline__ float fast_div(float a, float b, float r) {
   const float q = a * r;
-  const float rem = __builtin_fmaf(-q, b, a);
-  return __builtin_fmaf(rem, r, q);
+  const float nrem = __builtin_fmaf(q, b, -a);
+  return __builtin_fmaf(-nrem, r, q);
 }
 // QF_INFCHK 1: +-inf inputs are caught per element (max |a|).  2: they are caught once per client and
 // lane instead: an infinite a makes the fast quotient NaN (its residual is inf - inf), so the lane's
@@ -790,7 +792,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// q-FedAvg phase 1, second design (the default, QF_KERNEL 2): 2 waves per SIMD, the FedAvg chain fused
+// q-FedAvg phase 1, second design (QF_KERNEL / QF_CHAIN_KERNEL 2; measured slower, built off): 2 waves per SIMD
 // ------------------------------------------------------------------------------------------------
 // The first design (k_qfed_accum above) runs 1 wave per SIMD: `last`, the delta chain, the loaded row and
 // the quotients all live in registers (256 VGPRs + AGPR parking), so a wave has no loads in flight while

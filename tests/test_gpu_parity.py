@@ -303,10 +303,12 @@ def test_pickled_adapter_size_matches_reference(gpu_device):
     assert_state_equal(back.get_weights(), ours.get_weights(), "unpickled adapter")
 
 
+@pytest.mark.parametrize("last_zero", [0.0, -0.0])
 @pytest.mark.parametrize("lr", [0.05, 0.049, 0.1, 1 / 3, 7e-5, 123.456, 1e-20, 3e25])
-def test_qfed_division_is_correctly_rounded(gpu_device, lr):
+def test_qfed_division_is_correctly_rounded(gpu_device, lr, last_zero):
     """g = (L - W) / lr inside k_qfed_accum (constant-divisor division with one FMA correction) equals
-    IEEE fp32 division for values over the whole exponent range, zeros, denormals, inf and NaN."""
+    IEEE fp32 division for values over the whole exponent range, zeros of both signs, denormals, inf and
+    NaN.  With L = -0, L - W = a exactly, -0 included (L = +0 turns a = -0 into +0)."""
     from fedscale_amd import kernels as kx
 
     rng = np.random.default_rng(int(lr * 1e6) % 1000)
@@ -318,12 +320,13 @@ def test_qfed_division_is_correctly_rounded(gpu_device, lr):
     a[:16] = [0.0, -0.0, np.inf, -np.inf, np.nan, 1e-45, -1e-45, 1.1754944e-38, 3.4028235e38, -3.4028235e38,
               7.8886091e-31, 7.8886e-31, 1e30, 1.0000001e30, 1.0, -1.0]
     ld = n
-    x = torch.from_numpy(-a).cuda().view(1, ld)  # last = 0 -> L - W = a exactly
-    last = torch.zeros(ld, device="cuda")
+    x = torch.from_numpy(-a).cuda().view(1, ld)  # last = +-0 -> L - W = a exactly (but for a = -0)
+    last = torch.full((ld,), last_zero, device="cuda")
     delta = torch.empty(ld, device="cuda")
     sq = torch.zeros(1, dtype=torch.float64, device="cuda")
     with np.errstate(all="ignore"):
-        want = (np.float32(0) - (-a)) / np.float32(lr)  # the kernel's (L - W) with L = 0
+        want = (np.float32(last_zero) - (-a)) / np.float32(lr)  # the kernel's (L - W)
+    assert np.signbit(want[1]) == np.signbit(np.float32(last_zero))
     kx.qfed_accumulate(x, 1, n, last=last, alpha=torch.ones(1, device="cuda"), lr=lr, delta=delta, sqnorm=sq,
                        workspace=kx.qfed_workspace(1, "cuda"), accumulate=False)
     got = delta.cpu().numpy()
