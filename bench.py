@@ -268,7 +268,34 @@ def cpu_baseline_c1(seed: int, rounds: int = 50) -> dict:
         fedavg_close(acc, K)
         ts.append(time.perf_counter() - t0)
     ms = float(np.median(ts[5:])) * 1e3
-    return {"round_ms": ms, "client_updates_per_s": K / (ms * 1e-3), "cores": 1, "kind": "port"}
+    # the same round through the oracle's restatement of the reference loop: client_completion_handler's
+    # lines, update_weight_aggregation, set_weights (deepcopy + load_state_dict + update_round_gradient)
+    # and get_weights() — what the device leg's round covers (aggregator.py:454-511,
+    # torch_model_adapter.py:23-47)
+    import argparse
+
+    import torch
+
+    from oracle.cpu_reference import OracleAggregator, OracleModel, OracleModelAdapter, OracleServerOptimizer
+
+    names, shapes, base, _ = _c1_updates(seed, K)
+    args = argparse.Namespace(gradient_policy="fed-avg")
+    agg = OracleAggregator(OracleModelAdapter(OracleModel(names, [torch.from_numpy(b) for b in base]),
+                                              OracleServerOptimizer("fed-avg", args)), args)
+    th = []
+    for r in range(rounds + 5):
+        t0 = time.perf_counter()
+        agg.start_round(K)
+        for k in range(K):
+            agg.on_result({"client_id": k, "update_weight": ups[k], "moving_loss": 1.0})
+        agg.model_wrapper.get_weights()
+        th.append(time.perf_counter() - t0)
+    hms = float(np.median(th[5:])) * 1e3
+    return {"round_ms": ms, "client_updates_per_s": K / (ms * 1e-3), "cores": 1, "kind": "port",
+            "note": "round_ms: the reduction arithmetic alone (fedavg_step x K + fedavg_close)",
+            "handler_round_ms": hms,
+            "handler_note": "the reference loop's whole round as the device leg runs it: handler lines, "
+                            "update_weight_aggregation, set_weights, get_weights (oracle restatement)"}
 
 
 # ------------------------------------------------------------------------------------------------
