@@ -47,6 +47,17 @@ def cpu_shard_worker(rank, world, port, name):
         want = np.array([np.sum(((L[:full.P_full] - xf[k, :full.P_full]) / np.float32(0.05)) ** 2,
                                 dtype=np.float64) for k in range(K)])
         np.testing.assert_allclose(tot, want, rtol=1e-12)
+        # the same exchange in a fixed rank order (ShardGroup.sum_partials): ((p_0 + p_1) + p_2) + ... on
+        # every rank, bit for bit, whatever order the transport combines in
+        fixed = g.sum_partials(torch.from_numpy(part.copy())).numpy()
+        parts = g.collective_all_gather(torch.from_numpy(part.copy())).numpy().reshape(world, K)
+        acc = parts[0].copy()
+        for r in range(1, world):
+            acc = acc + parts[r]
+        np.testing.assert_array_equal(fixed, acc)
+        everyone = g.collective_all_gather(torch.from_numpy(fixed.copy())).numpy().reshape(world, K)
+        assert (everyone == everyone[0]).all()
+        np.testing.assert_allclose(fixed, want, rtol=1e-12)
     finally:
         dist.destroy_process_group()
 
