@@ -116,6 +116,7 @@ struct RedArgs {
   int64_t P4;   // float4 columns to produce (ceil(P/4))
   int64_t col0; // first float4 column of this launch (a launch covers [col0, min(P4, col0 + ntiles*span)))
   int64_t ntiles;  // tiles of this launch; workgroup b takes tiles b, b + grid, ...
+  int sw;          // strips (64 float4 columns) per wave per tile, <= the variant's V
   int K;
   int flags;
   const float* a;
@@ -137,15 +138,17 @@ struct RedArgs {
 #ifndef FA_RED_WAVES
 #define FA_RED_WAVES 4
 #endif
-// One tile: the workgroup's FA_RED_WAVES waves each own 64*V float4 columns and walk all K clients.
+// One tile: the workgroup's FA_RED_WAVES waves each own 64*sw float4 columns (sw <= V strips, a run-time
+// width) and walk all K clients.
 template <int V, int U, int EPI, bool W>
 __device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int lane, int wave) {
   const f4* __restrict__ xp = reinterpret_cast<const f4*>(r.x);
-  const int64_t c0 = r.col0 + (tile * FA_RED_WAVES + wave) * (64 * V) + lane;
+  const int sw = r.sw;
+  const int64_t c0 = r.col0 + (tile * FA_RED_WAVES + wave) * (64LL * sw) + lane;
 
   bool ok[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) ok[j] = (c0 + 64 * j) < r.P4;
+  for (int j = 0; j < V; ++j) ok[j] = j < sw && (c0 + 64 * j) < r.P4;
 
   f4 s[V];
   int k = 0;
@@ -310,6 +313,7 @@ template <int V, int U, int EPI, bool W>
 static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_waves_only, int64_t cap,
                             hipStream_t st) {
   const int64_t span = 64LL * FA_RED_WAVES * V;
+  r.sw = V;
   int64_t nblk = (col_end - col + span - 1) / span;
   if (full_waves_only) {
     const int64_t R = resident_blocks<V, U, EPI, W>();
@@ -332,6 +336,41 @@ static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_w
   return (full_waves_only && end < col_end) ? end : col_end;
 }
 
+// Balanced launches (run-time tile width sw strips per wave, sw <= the variant's V; every workgroup gets
+// the same number of equally wide tiles, the last tile ragged):
+//  * one round when the bucket fits ~FA_BAL_GRID workgroups (per 256 CUs) at sw <= 32: one tile per
+//    workgroup, on the narrowest variant that holds sw strips — a narrower tile brings more clients in
+//    flight (V x U = 32 KiB per wave), so every workgroup keeps a full load queue whatever the width;
+//  * otherwise R rounds of the capped grid (FA_GRID_CAP_PCT of the CUs, V = 32), each workgroup walking R
+//    tiles of width sw = ceil(strips / (waves x R x grid)): the old capped plan used full-width tiles
+//    only, so a bucket just over one round of them left half the cap idle for two rounds.
+// Measured (profiles/r02_tune_small_p.log), 1000 clients: 3.125 M (config 4's bucket over 8 GPUs, the
+// north star's per-GPU work at 8 GPUs) 6.20 -> 7.18 TB/s; 8 M 5.76 -> 6.8; 5.5 M 6.99 -> 7.18; 2 M
+// 6.44 -> 6.91; 1 M 6.64 -> 6.85; 6.25 M and above unchanged.  Short rounds (K x sw < FA_BAL_MIN_WORK,
+// e.g. config 2's 100 x 1 M) and narrow buckets (sw < FA_BAL_MIN_SW) read faster with the level cascade
+// below (more, narrower workgroups).
+#ifndef FA_BAL_GRID
+#define FA_BAL_GRID 224
+#endif
+#ifndef FA_BAL_MIN_SW
+#define FA_BAL_MIN_SW 5
+#endif
+#ifndef FA_BAL_MIN_WORK
+#define FA_BAL_MIN_WORK 1000  // K x sw: KiB one wave reads over the round
+#endif
+template <int V, int U, int EPI, bool W>
+static void launch_balanced(RedArgs r, int64_t sw, int64_t rounds, hipStream_t st) {
+  const int64_t S = (r.P4 + 63) / 64;
+  r.col0 = 0;
+  r.sw = (int)sw;
+  r.ntiles = (S + (int64_t)FA_RED_WAVES * sw - 1) / ((int64_t)FA_RED_WAVES * sw);
+  const int64_t grid = (r.ntiles + rounds - 1) / rounds;
+  if (grid < r.ntiles)
+    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, true>), dim3((unsigned)grid), dim3(64 * FA_RED_WAVES), 0, st, r);
+  else
+    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, false>), dim3((unsigned)r.ntiles), dim3(64 * FA_RED_WAVES), 0, st, r);
+}
+
 template <int EPI, bool W>
 static void launch_plan(const RedArgs& r, hipStream_t st) {
   int64_t col = 0;
@@ -345,6 +384,29 @@ static void launch_plan(const RedArgs& r, hipStream_t st) {
   const int64_t cap = (int64_t)cu_count() * FA_GRID_CAP_PCT / 100;
   const int64_t span0 = 64LL * FA_RED_WAVES * FA_L0_V;
   const int64_t tiles0 = (r.P4 + span0 - 1) / span0;
+#if FA_BAL_GRID > 0
+  {
+    const int64_t S = (r.P4 + 63) / 64;
+    const int64_t gb = (int64_t)cu_count() * FA_BAL_GRID / 256;
+    const int64_t sw1 = gb > 0 ? (S + (int64_t)FA_RED_WAVES * gb - 1) / ((int64_t)FA_RED_WAVES * gb) : 0;
+    if (gb > 0 && cap > 0 && sw1 > 32) {  // R rounds of the capped grid
+      const int64_t per_round = (int64_t)FA_RED_WAVES * 32 * cap;
+      const int64_t R = (S + per_round - 1) / per_round;
+      const int64_t sw = (S + (int64_t)FA_RED_WAVES * R * cap - 1) / ((int64_t)FA_RED_WAVES * R * cap);
+      launch_balanced<32, 1, EPI, W>(r, sw, R, st);
+      return;
+    }
+    if (sw1 >= FA_BAL_MIN_SW && (int64_t)r.K * sw1 >= FA_BAL_MIN_WORK) {  // one round
+      if (sw1 > 16)
+        launch_balanced<32, 1, EPI, W>(r, sw1, 1, st);
+      else if (sw1 > 8)
+        launch_balanced<16, 2, EPI, W>(r, sw1, 1, st);
+      else
+        launch_balanced<8, 4, EPI, W>(r, sw1, 1, st);
+      return;
+    }
+  }
+#endif
   if (cap > 0 && tiles0 * 20 >= cap * 17) {  // enough widest tiles to keep ~cap workgroups busy
     launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, 0, r.P4, false, cap, st);
     return;

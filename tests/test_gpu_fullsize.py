@@ -196,3 +196,54 @@ def test_c2_through_the_drop_in_from_host_updates(gpu_device):
     want = fedavg_close(acc, K)
     for got, w in zip(agg.model_wrapper.get_weights(), want):
         np.testing.assert_array_equal(got.numpy(), w)
+
+
+@pytest.mark.parametrize("K,P,weighted", [
+    (200, 1_000_003, False),    # one round, sw 5 (V = 8 variant), K x sw at the threshold
+    (200, 2_300_001, True),     # one round, sw 11 (V = 16), FedBuff weights
+    (1000, 3_125_056, False),   # the north star's per-GPU bucket at 8 GPUs (config 4's 25M / 8), sw 14
+    (100, 5_000_001, False),    # one round, sw 22 (V = 32)
+    (60, 9_000_001, True),      # two rounds of the capped grid at sw 23 (LOOP kernel, run-time width)
+])
+def test_reduce_balanced_plans_bit_exact(gpu_device, K, P, weighted):
+    """The balanced launch plans of fa_reduce (run-time tile width, fedagg.hip launch_plan): every column
+    reduced by one thread in arrival order, so bit-exact to the sequential fp32 chain, with the sample
+    taken around every tile boundary of the plan."""
+    from fedscale_amd import kernels as kx
+    from fedscale_amd import synth
+    from fedscale_amd.bucket import round_up
+
+    seed = 300 + K
+    ld = round_up(P, 64)
+    x = torch.empty(K, ld, device="cuda")
+    synth.fill(x, K, P, seed=seed)
+    f = np.float32
+    w = (np.random.default_rng(K).uniform(0.2, 1.0, size=K).astype(f) if weighted else None)
+    out = torch.empty(ld, device="cuda")
+    denom = float(f(w.sum())) if weighted else float(f(K))
+    kx.reduce(x, K, P, out, a=torch.from_numpy(w).cuda() if weighted else None, denom=denom, finalize=True)
+    # tile boundaries of the plan (4 waves x sw strips of 64 float4 per tile)
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    S = (ld // 4 + 63) // 64
+    gb = cus * 224 // 256
+    sw1 = -(-S // (4 * gb))
+    if sw1 > 32:
+        cap = cus * 75 // 100
+        R = -(-S // (4 * 32 * cap))
+        sw = -(-S // (4 * R * cap))
+    else:
+        sw = sw1
+    span = 4 * sw * 64 * 4  # floats per tile
+    bounds = np.arange(span, P, span)
+    cols = np.unique(np.concatenate([_sample_cols(P, n=2048, seed=K),
+                                     np.clip(np.concatenate([bounds - 1, bounds]), 0, P - 1)]))
+    acc = None
+    for c0 in range(0, K, 100):
+        xs = synth.host_columns(seed, range(c0, min(K, c0 + 100)), cols)
+        for i, row in enumerate(xs):
+            k = c0 + i
+            t = row * w[k] if weighted else row
+            acc = t if acc is None else acc + t
+    want = np.divide(acc, f(denom))
+    np.testing.assert_array_equal(out[torch.from_numpy(cols).cuda()].cpu().numpy(), want)
+    del x
