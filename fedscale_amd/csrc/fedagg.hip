@@ -139,16 +139,16 @@ struct RedArgs {
 #define FA_RED_WAVES 4
 #endif
 // One tile: the workgroup's FA_RED_WAVES waves each own 64*sw float4 columns (sw <= V strips, a run-time
-// width) and walk all K clients.
-template <int V, int U, int EPI, bool W>
+// width; FULL: sw == V, the compile-time width) and walk all K clients.
+template <int V, int U, int EPI, bool W, bool FULL>
 __device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int lane, int wave) {
   const f4* __restrict__ xp = reinterpret_cast<const f4*>(r.x);
-  const int sw = r.sw;
+  const int sw = FULL ? V : r.sw;
   const int64_t c0 = r.col0 + (tile * FA_RED_WAVES + wave) * (64LL * sw) + lane;
 
   bool ok[V];
 #pragma unroll
-  for (int j = 0; j < V; ++j) ok[j] = j < sw && (c0 + 64 * j) < r.P4;
+  for (int j = 0; j < V; ++j) ok[j] = (FULL || j < sw) && (c0 + 64 * j) < r.P4;
 
   f4 s[V];
   int k = 0;
@@ -228,7 +228,8 @@ __device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int 
 
 // LOOP = false: workgroup b reduces tile b (grid = tiles).  LOOP = true: a capped grid, workgroup b
 // reduces tiles b, b + grid, ... (r.ntiles in this launch): fewer concurrent column streams per round.
-template <int V, int U, int EPI, bool W, bool LOOP>
+// FULL: the tiles are V strips wide (r.sw == V, compile-time masks); otherwise r.sw < V at run time.
+template <int V, int U, int EPI, bool W, bool LOOP, bool FULL = true>
 __global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -242,9 +243,9 @@ __global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
       b = x * q + (x < rem ? x : rem) + b / 8;
     }
 #endif
-    for (int64_t tile = b; tile < r.ntiles; tile += gridDim.x) reduce_tile<V, U, EPI, W>(r, tile, lane, wave);
+    for (int64_t tile = b; tile < r.ntiles; tile += gridDim.x) reduce_tile<V, U, EPI, W, FULL>(r, tile, lane, wave);
   } else {
-    reduce_tile<V, U, EPI, W>(r, blockIdx.x, lane, wave);
+    reduce_tile<V, U, EPI, W, FULL>(r, blockIdx.x, lane, wave);
   }
 }
 
@@ -337,18 +338,19 @@ static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_w
 }
 
 // Balanced launches (run-time tile width sw strips per wave, sw <= the variant's V; every workgroup gets
-// the same number of equally wide tiles, the last tile ragged):
-//  * one round when the bucket fits ~FA_BAL_GRID workgroups (per 256 CUs) at sw <= 32: one tile per
-//    workgroup, on the narrowest variant that holds sw strips — a narrower tile brings more clients in
-//    flight (V x U = 32 KiB per wave), so every workgroup keeps a full load queue whatever the width;
-//  * otherwise R rounds of the capped grid (FA_GRID_CAP_PCT of the CUs, V = 32), each workgroup walking R
-//    tiles of width sw = ceil(strips / (waves x R x grid)): the old capped plan used full-width tiles
-//    only, so a bucket just over one round of them left half the cap idle for two rounds.
-// Measured (profiles/r02_tune_small_p.log), 1000 clients: 3.125 M (config 4's bucket over 8 GPUs, the
-// north star's per-GPU work at 8 GPUs) 6.20 -> 7.18 TB/s; 8 M 5.76 -> 6.8; 5.5 M 6.99 -> 7.18; 2 M
-// 6.44 -> 6.91; 1 M 6.64 -> 6.85; 6.25 M and above unchanged.  Short rounds (K x sw < FA_BAL_MIN_WORK,
-// e.g. config 2's 100 x 1 M) and narrow buckets (sw < FA_BAL_MIN_SW) read faster with the level cascade
-// below (more, narrower workgroups).
+// the same number of equally wide tiles, the last tile ragged).  With S strips of 64 float4 columns:
+//  * sw1 = ceil(S / (waves x cap)) > 32 (cap = FA_GRID_CAP_PCT of the CUs): R rounds of the capped grid,
+//    R = ceil(S / (waves x 32 x cap)), sw = ceil(S / (waves x R x cap)) — the round-1 capped plan at
+//    1000 x 25 M exactly; round 1 used full-width tiles only, so a bucket just above one round of them
+//    (6.3-8.4 M) ran two rounds on half the cap;
+//  * 8 <= sw1 <= 32: one round of sw1-wide tiles, one per workgroup, on ~cap workgroups;
+//  * narrower: one round on ~FA_BAL_GRID workgroups per 256 CUs, unless the tiles would be narrower than
+//    FA_BAL_MIN_SW or the round short (K x sw < FA_BAL_MIN_WORK): then the level cascade below (more,
+//    narrower workgroups) reads faster;
+//  * rounds of fewer than FA_BAL_SHORT_K clients take one round over every CU whenever sw <= 32.
+// One-round launches use the narrowest variant that holds sw (V x U = 32 KiB of loads in flight per
+// wave).  Measured: profiles/r02_tune_small_p.log (1000 x 3.125 M, config 4's bucket over 8 GPUs and the
+// north star's per-GPU work at 8 GPUs: 6.2 -> 7.0 TB/s).
 #ifndef FA_BAL_GRID
 #define FA_BAL_GRID 224
 #endif
@@ -358,6 +360,9 @@ static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_w
 #ifndef FA_BAL_MIN_WORK
 #define FA_BAL_MIN_WORK 1000  // K x sw: KiB one wave reads over the round
 #endif
+#ifndef FA_BAL_SHORT_K
+#define FA_BAL_SHORT_K 200  // rounds of fewer clients: one round over every CU when the tiles fit
+#endif
 template <int V, int U, int EPI, bool W>
 static void launch_balanced(RedArgs r, int64_t sw, int64_t rounds, hipStream_t st) {
   const int64_t S = (r.P4 + 63) / 64;
@@ -365,10 +370,17 @@ static void launch_balanced(RedArgs r, int64_t sw, int64_t rounds, hipStream_t s
   r.sw = (int)sw;
   r.ntiles = (S + (int64_t)FA_RED_WAVES * sw - 1) / ((int64_t)FA_RED_WAVES * sw);
   const int64_t grid = (r.ntiles + rounds - 1) / rounds;
-  if (grid < r.ntiles)
-    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, true>), dim3((unsigned)grid), dim3(64 * FA_RED_WAVES), 0, st, r);
-  else
-    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, false>), dim3((unsigned)r.ntiles), dim3(64 * FA_RED_WAVES), 0, st, r);
+  const dim3 blk(64 * FA_RED_WAVES);
+  if (grid < r.ntiles) {
+    if (sw == V)
+      hipLaunchKernelGGL((k_reduce<V, U, EPI, W, true, true>), dim3((unsigned)grid), blk, 0, st, r);
+    else
+      hipLaunchKernelGGL((k_reduce<V, U, EPI, W, true, false>), dim3((unsigned)grid), blk, 0, st, r);
+  } else if (sw == V) {
+    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, false, true>), dim3((unsigned)r.ntiles), blk, 0, st, r);
+  } else {
+    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, false, false>), dim3((unsigned)r.ntiles), blk, 0, st, r);
+  }
 }
 
 template <int EPI, bool W>
@@ -385,24 +397,32 @@ static void launch_plan(const RedArgs& r, hipStream_t st) {
   const int64_t span0 = 64LL * FA_RED_WAVES * FA_L0_V;
   const int64_t tiles0 = (r.P4 + span0 - 1) / span0;
 #if FA_BAL_GRID > 0
-  {
+  if (cap > 0) {
     const int64_t S = (r.P4 + 63) / 64;
-    const int64_t gb = (int64_t)cu_count() * FA_BAL_GRID / 256;
-    const int64_t sw1 = gb > 0 ? (S + (int64_t)FA_RED_WAVES * gb - 1) / ((int64_t)FA_RED_WAVES * gb) : 0;
-    if (gb > 0 && cap > 0 && sw1 > 32) {  // R rounds of the capped grid
+    const int64_t g1 = r.K < FA_BAL_SHORT_K ? (int64_t)cu_count() : cap;  // short rounds: one round, all CUs
+    const int64_t sw1 = (S + (int64_t)FA_RED_WAVES * g1 - 1) / ((int64_t)FA_RED_WAVES * g1);
+    if (sw1 > 32) {  // R rounds of the capped grid
       const int64_t per_round = (int64_t)FA_RED_WAVES * 32 * cap;
       const int64_t R = (S + per_round - 1) / per_round;
       const int64_t sw = (S + (int64_t)FA_RED_WAVES * R * cap - 1) / ((int64_t)FA_RED_WAVES * R * cap);
       launch_balanced<32, 1, EPI, W>(r, sw, R, st);
       return;
     }
-    if (sw1 >= FA_BAL_MIN_SW && (int64_t)r.K * sw1 >= FA_BAL_MIN_WORK) {  // one round
+    if (sw1 >= 8) {  // one round of wide tiles on (about) the capped grid
       if (sw1 > 16)
         launch_balanced<32, 1, EPI, W>(r, sw1, 1, st);
-      else if (sw1 > 8)
-        launch_balanced<16, 2, EPI, W>(r, sw1, 1, st);
       else
-        launch_balanced<8, 4, EPI, W>(r, sw1, 1, st);
+        launch_balanced<16, 2, EPI, W>(r, sw1, 1, st);
+      return;
+    }
+    // narrow tiles: one round on more workgroups, unless the round is short
+    const int64_t gb = (int64_t)cu_count() * FA_BAL_GRID / 256;
+    const int64_t swb = (S + (int64_t)FA_RED_WAVES * gb - 1) / ((int64_t)FA_RED_WAVES * gb);
+    if (swb >= FA_BAL_MIN_SW && (int64_t)r.K * swb >= FA_BAL_MIN_WORK) {
+      if (swb > 8)
+        launch_balanced<16, 2, EPI, W>(r, swb, 1, st);
+      else
+        launch_balanced<8, 4, EPI, W>(r, swb, 1, st);
       return;
     }
   }

@@ -14,6 +14,7 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+YOGI = os.environ.get("TUNE_YOGI") == "1"  # time fa_reduce_yogi (FedYoGi fused) instead of fa_reduce
 
 
 def main():
@@ -40,10 +41,16 @@ def run(K, P, rounds):
     for path in sorted(glob.glob(os.path.join(ROOT, "fedscale_amd", "variants", "*.so"))) + [
             os.path.join(ROOT, "fedscale_amd", "libfedagg.so")]:
         lib = ctypes.CDLL(path)
-        f = lib.fa_reduce
+        if YOGI:
+            f = lib.fa_reduce_yogi
+            vp, fl = ctypes.c_void_p, ctypes.c_float
+            f.argtypes = [vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, vp, vp, fl, vp, vp, vp, vp, vp,
+                          fl, fl, fl, fl, fl, ctypes.c_int32, vp]
+        else:
+            f = lib.fa_reduce
+            f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
+                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_int32, ctypes.c_void_p]
         f.restype = ctypes.c_int32
-        f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32, ctypes.c_int64, ctypes.c_void_p,
-                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_float, ctypes.c_int32, ctypes.c_void_p]
         libs[os.path.basename(path)] = f
     ld = round_up(P, 64)
     x = torch.empty(K, ld, device="cuda")
@@ -51,6 +58,13 @@ def run(K, P, rounds):
     out = torch.empty(ld, device="cuda")
     ref = None
     st = torch.cuda.current_stream().cuda_stream
+    if YOGI:  # fused FedYoGi epilogue (fa_reduce_yogi), m/v re-initialised by every call (FA_YOGI_INIT)
+        last, m, v = (torch.zeros(ld, device="cuda") for _ in range(3))
+        plain = {n: f for n, f in libs.items()}
+        for n, f0 in plain.items():
+            libs[n] = (lambda f0: lambda xp, ld_, K_, P_, a, acc, outp, den, fl, s_: f0(
+                xp, ld_, K_, P_, None, None, den, last.data_ptr(), m.data_ptr(), v.data_ptr(), outp, None,
+                3e-3, 1e-8, 0.9, 0.1, 0.01, fl | 4, s_))(f0)
     times = {n: [] for n in libs}
     for r in range(rounds):
         for n, f in libs.items():
@@ -67,7 +81,7 @@ def run(K, P, rounds):
                 ref = out.clone()
             else:
                 assert torch.equal(out, ref), f"{n} result differs"
-    bytes_ = 4 * K * P + 4 * P
+    bytes_ = 4 * K * P + (24 * P if YOGI else 4 * P)
     res = {n: {"median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
                "GBps": bytes_ / (np.median(t) * 1e-3) / 1e9} for n, t in times.items()}
     print(f"--- K={K} P={P}", flush=True)
