@@ -43,7 +43,7 @@ def run(K, rounds, which, n_parts):
                 up[n] = np.array(rng.integers(0, 100), dtype=np.int64).reshape(s)
         pool.append(up)
     t_add, t_fin = [], []
-    for r in range(rounds + 1):
+    for r in range(rounds + 2):
         torch.cuda.synchronize()
         agg.start_round(K)
         t0 = time.perf_counter()
@@ -53,7 +53,7 @@ def run(K, rounds, which, n_parts):
         agg.on_result({"client_id": K - 1, "update_weight": pool[(K - 1) % 4], "moving_loss": 1.0})
         adapter.get_weights()
         t2 = time.perf_counter()
-        if r > 0:
+        if r > 1:  # two warm-up rounds: staging, pinned rows and both egress snapshots allocated
             t_add.append((t1 - t0) / (K - 1))
             t_fin.append(t2 - t1)
     P = sum(int(np.prod(s)) for s, d in zip(shapes, dtypes) if d == torch.float32)
@@ -67,8 +67,11 @@ def main():
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 3
     which = sys.argv[3] if len(sys.argv) > 3 else "femnist"
     parts = [int(p) for p in sys.argv[4].split(",")] if len(sys.argv) > 4 else [0, 1, 2, 4, 8]
+    import gc
+
     for n in parts:
         print(json.dumps(run(K, rounds, which, n)), flush=True)
+        gc.collect()
         torch.cuda.empty_cache()
 
 
