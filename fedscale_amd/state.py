@@ -22,6 +22,8 @@ benchmark and tests), with two ways to spread a round over the ranks (SURVEY §8
 """
 from __future__ import annotations
 
+import atexit
+import weakref
 from dataclasses import dataclass
 from typing import Optional
 
@@ -158,6 +160,18 @@ class PartOf(ShardGroup):
         raise RuntimeError("in-process shard: the coordinating adapter combines the parts")
 
 
+def _close_live_groups():
+    for g in list(_LIVE_GROUPS):
+        try:
+            g.close()
+        except Exception:
+            pass
+
+
+_LIVE_GROUPS: "weakref.WeakSet" = weakref.WeakSet()
+atexit.register(_close_live_groups)
+
+
 class DeviceGroup:
     """The GPUs ONE aggregator process drives (FedScale's aggregator is a single process, aggregator.py:
     177-192, 919-963).  Cross-device steps are RCCL collectives over xGMI issued for every device at once
@@ -200,6 +214,7 @@ class DeviceGroup:
             h = ctypes.c_void_p()
             _native.call("fa_rccl_init", self.world, devs, ctypes.byref(h))
             self._comm = h
+            _LIVE_GROUPS.add(self)  # destroyed at interpreter exit while the HIP runtime is still up
         return self._comm
 
     def close(self):
@@ -207,9 +222,14 @@ class DeviceGroup:
             from . import _native
 
             comm, self._comm = self._comm, None
+            _LIVE_GROUPS.discard(self)
             _native.call("fa_rccl_destroy", comm)
 
     def __del__(self):
+        import sys
+
+        if sys.is_finalizing():  # too late to call into RCCL safely; _close_live_groups ran at exit
+            return
         try:
             self.close()
         except Exception:

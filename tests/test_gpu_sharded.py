@@ -333,6 +333,28 @@ def test_rccl_collectives_one_gpu(gpu_device):
     g.close()
 
 
+def test_rccl_communicator_left_open_at_exit(gpu_device):
+    """A ShardedModelAdapter that is never closed (the aggregator process simply exits): its RCCL
+    communicator is destroyed by the exit hook while the HIP runtime is still up, and the process exits 0."""
+    import os
+    import subprocess
+    import sys
+
+    code = (
+        "import torch\n"
+        "from fedscale_amd.state import DeviceGroup\n"
+        "g = DeviceGroup([0], transport='rccl')\n"
+        "x = torch.ones(64, dtype=torch.float64, device='cuda:0')\n"
+        "g.sum_f64([x])\n"
+        "torch.cuda.synchronize()\n"
+        "assert float(x.sum()) == 64.0\n"
+        "print('ok', flush=True)\n"
+    )
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "ok" in r.stdout, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+
+
 def test_nccl_process_group_collectives_world1(gpu_device):
     """The torch.distributed (RCCL) branch of ShardGroup with device tensors, at world size 1 on the box:
     all_gather_into_tensor and all_reduce run through the nccl backend (the N-GPU SPMD bench uses them)."""
