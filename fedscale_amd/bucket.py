@@ -243,6 +243,7 @@ class ClientStaging:
         self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self.capacity = int(capacity)
         self.generation = 0  # bumped by every DeviceRound that takes the slots over
+        self.side_scratch = None  # (int64, float64) side-table sums of FedAvg / FedBuff rounds, reused
         self.x = torch.zeros(self.capacity, layout.ld, dtype=torch.float32, device=self.device)
         self.xi = torch.zeros(self.capacity, layout.ldq, dtype=torch.int64, device=self.device)
         self._ring = []  # pinned rows for host updates, allocated on the first one (a part of a sharded

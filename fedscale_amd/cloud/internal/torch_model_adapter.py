@@ -84,13 +84,25 @@ class EgressHandle:
         return (list, (list(self.weights()),))
 
 
+class _HostBuf:
+    """Pinned host buffers for one model version (fp32 bucket ``f``, side table ``s``) with their state_dict
+    views, made once: buffers are pooled across versions, so egress clones from ready-made views."""
+
+    __slots__ = ("f", "s", "views")
+
+    def __init__(self, layout: BucketLayout):
+        self.f = torch.empty(max(1, layout.P_full), dtype=torch.float32, pin_memory=True)
+        self.s = torch.empty(max(1, layout.Q), dtype=torch.int64)
+        self.views = layout.unpack(self.f, self.s)
+
+
 class _HostSnapshot:
-    """Pinned host copy of one model version (fp32 bucket ``f``, side table ``s``) and its reader count."""
+    """One model version's host copy (a ``_HostBuf``) and its reader count."""
 
-    __slots__ = ("version", "f", "s", "readers")
+    __slots__ = ("version", "buf", "readers")
 
-    def __init__(self, version, f, s):
-        self.version, self.f, self.s, self.readers = version, f, s, 0
+    def __init__(self, version, buf: _HostBuf):
+        self.version, self.buf, self.readers = version, buf, 0
 
 
 def _resolve_device(device) -> torch.device:
@@ -209,7 +221,10 @@ class TorchModelAdapter(ModelAdapterBase):
         if torch.cuda.current_stream(self.device) != self._ready_stream:
             self._ready.synchronize()  # another stream wrote the model: the blocking copy alone would not wait
         full = self.shards.all_gather(self._f[self._cur])
-        f_cpu[:L.P_full].copy_(full[:L.P_full])
+        if L.P_full == f_cpu.numel():  # (a _HostBuf holds exactly P_full floats, at least one)
+            f_cpu.copy_(full[:L.P_full])
+        else:
+            f_cpu[:L.P_full].copy_(full[:L.P_full])
         if L.Q:
             s_cpu[:L.Q].copy_(self._s[self._cur][:L.Q])
 
@@ -220,15 +235,12 @@ class TorchModelAdapter(ModelAdapterBase):
         with self._egress_lock:
             snap = self._snap
             if snap is None or snap.version != self._version:
-                L = self.layout
-                f = self._snap_pool.pop() if self._snap_pool else torch.empty(max(1, L.P_full), dtype=torch.float32,
-                                                                              pin_memory=True)
-                s_cpu = torch.empty(max(1, L.Q), dtype=torch.int64)
-                self._copy_to_host(f, s_cpu)
-                old, snap = snap, _HostSnapshot(self._version, f, s_cpu)
+                buf = self._snap_pool.pop() if self._snap_pool else _HostBuf(self.layout)
+                self._copy_to_host(buf.f, buf.s)
+                old, snap = snap, _HostSnapshot(self._version, buf)
                 self._snap = snap
                 if old is not None and old.readers == 0:
-                    self._snap_pool.append(old.f)
+                    self._snap_pool.append(old.buf)
             snap.readers += 1
             return snap
 
@@ -236,10 +248,10 @@ class TorchModelAdapter(ModelAdapterBase):
         with self._egress_lock:
             snap.readers -= 1
             if snap.readers == 0 and snap is not self._snap:
-                self._snap_pool.append(snap.f)
+                self._snap_pool.append(snap.buf)
 
     def _clone_weights(self, snap: "_HostSnapshot") -> list:
-        return [t.clone() for t in self.layout.unpack(snap.f, snap.s)]
+        return [t.clone() for t in snap.buf.views]
 
     def get_weights(self) -> List[torch.Tensor]:
         """torch_model_adapter.py:41-47: cloned CPU tensors in state_dict order (gathers the shards).

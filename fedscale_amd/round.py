@@ -77,9 +77,16 @@ class DeviceRound:
         self.acc = None  # running fp32 chain across chunks
         # int64 / float64 side sums: the first chunk's accumulate overwrites them, so no memset is needed
         # unless a client-mode rank may contribute nothing to the cross-rank sum
-        alloc = torch.zeros if self.cg is not None else torch.empty
-        self.acc_i = alloc(L.ldq, dtype=torch.int64, device=dev)
-        self.acc_d = alloc(L.ldq, dtype=torch.float64, device=dev)
+        if self.cg is None and policy in ("fedavg", "fedbuff"):
+            # consumed by finalize_mean before the next round can begin: one pair per staging, reused
+            if self.staging.side_scratch is None:
+                self.staging.side_scratch = (torch.empty(L.ldq, dtype=torch.int64, device=dev),
+                                             torch.empty(L.ldq, dtype=torch.float64, device=dev))
+            self.acc_i, self.acc_d = self.staging.side_scratch
+        else:  # q-FedAvg keeps them for the round's lazily computed mean (mean_from_staging)
+            alloc = torch.zeros if self.cg is not None else torch.empty
+            self.acc_i = alloc(L.ldq, dtype=torch.int64, device=dev)
+            self.acc_d = alloc(L.ldq, dtype=torch.float64, device=dev)
         self._w32 = np.zeros(self.cap, dtype=np.float32)  # per-slot weights of the current chunk
         self._w64 = np.zeros(self.cap, dtype=np.float64)
         self.last_f32, self.last_i64 = last_f32, last_i64
