@@ -85,6 +85,7 @@ class ShardedModelAdapter(TorchModelAdapter):
         self._next_row = 0
         self.pack_workers = default_pack_workers()
         self._init_egress(True)
+        self._egress_src = self._part_buffers()
 
     def __reduce__(self):
         return (self.__class__, (self.get_model(), self.optimizer, [d.index for d in self.group.devices], None,
@@ -136,8 +137,14 @@ class ShardedModelAdapter(TorchModelAdapter):
         for p, r in zip(self.parts, rnd.rounds):
             p._finish_qfed(r)
 
+    def _part_buffers(self):
+        return [(p._f[p._cur], p._s[p._cur]) for p in self.parts]
+
     def _commit(self):
+        """The parts have committed their new buffers one by one; the model version and the buffers egress
+        reads change together here, so a servicer thread never snapshots a mix of old and new parts."""
         with self._egress_lock:
+            self._egress_src = self._part_buffers()
             self._version += 1
 
     # ---- reference API ----------------------------------------------------------------------------
@@ -162,14 +169,17 @@ class ShardedModelAdapter(TorchModelAdapter):
         self._commit()
 
     def _copy_to_host(self, f_cpu: torch.Tensor, s_cpu: torch.Tensor):
-        """Per-part D2H into the pinned snapshot (each over its own device's link); no collective."""
+        """Per-part D2H into the pinned snapshot (each over its own device's link); no collective.  Reads
+        the buffers of the committed version (``_egress_src``, swapped with ``_version`` under the egress
+        lock the caller holds), not the parts' live pointers, which flip one part at a time."""
         for p in self.parts:
-            p._ready.synchronize()  # every part's round, whatever stream it ran on
-        for p in self.parts:
+            p._ready.synchronize()  # every part's writes, whatever stream they ran on
+        src = self._egress_src
+        for p, (f_dev, _) in zip(self.parts, src):
             L = p.layout
             if L.P:
-                f_cpu[L.p0:L.p1].copy_(p._f[p._cur][:L.P], non_blocking=True)
-        s_cpu[:self.layout.Q].copy_(self.parts[0]._s[self.parts[0]._cur][:self.layout.Q])
+                f_cpu[L.p0:L.p1].copy_(f_dev[:L.P], non_blocking=True)
+        s_cpu[:self.layout.Q].copy_(src[0][1][:self.layout.Q])
         for p in self.parts:
             torch.cuda.current_stream(p.device).synchronize()
 
