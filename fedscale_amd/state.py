@@ -23,6 +23,7 @@ benchmark and tests), with two ways to spread a round over the ranks (SURVEY §8
 from __future__ import annotations
 
 import atexit
+import sys
 import weakref
 from dataclasses import dataclass
 from typing import Optional
@@ -226,11 +227,9 @@ class DeviceGroup:
             _native.call("fa_rccl_destroy", comm)
 
     def __del__(self):
-        import sys
-
-        if sys.is_finalizing():  # too late to call into RCCL safely; _close_live_groups ran at exit
-            return
         try:
+            if sys.is_finalizing():  # too late to call into RCCL safely; _close_live_groups ran at exit
+                return
             self.close()
         except Exception:
             pass
