@@ -247,3 +247,44 @@ def test_reduce_balanced_plans_bit_exact(gpu_device, K, P, weighted):
     want = np.divide(acc, f(denom))
     np.testing.assert_array_equal(out[torch.from_numpy(cols).cuda()].cpu().numpy(), want)
     del x
+
+
+@pytest.mark.parametrize("K,P", [(200, 2_300_001), (150, 5_000_001), (1000, 3_125_056)])
+def test_reduce_yogi_balanced_plans_bit_exact(gpu_device, K, P):
+    """The fused FedYoGi epilogue on the balanced plans' run-time-width tiles (V = 16 and V = 32 variants
+    with sw < V): mean, m, v and the new model bit-exact to the IEEE numpy restatement, two rounds."""
+    from fedscale_amd import kernels as kx
+    from fedscale_amd import synth
+    from fedscale_amd.bucket import round_up
+
+    seed = 700 + K
+    ld = round_up(P, 64)
+    f = np.float32
+    hp = dict(eta=float(f(3e-3)), tau=float(f(1e-8)), beta=float(f(0.9)), omb=float(f(1.0 - 0.9)),
+              omb2=float(f(1.0 - 0.99)))
+    x = torch.empty(K, ld, device="cuda")
+    synth.fill(x, K, P, seed=seed)
+    last = torch.empty(1, ld, device="cuda")
+    synth.fill(last, 1, P, seed=seed + 5000, scale_noise=0.0)
+    last = last[0]
+    m, v, out, mean = (torch.empty(ld, device="cuda") for _ in range(4))
+    cols = _sample_cols(P, n=2048, seed=K)
+    ci = torch.from_numpy(cols).cuda()
+    L = last[ci].cpu().numpy()
+    mh = np.zeros(len(cols), f)
+    vh = np.full(len(cols), f(hp["tau"]))
+    cur = np.divide(_host_seq_sum(seed, K, cols), K)
+    for r in range(2):
+        kx.reduce_yogi(x, K, P, last=last, m=m, v=v, out=out, denom=float(f(K)), init=(r == 0), mean_out=mean, **hp)
+        g = cur - L
+        g2 = g * g
+        mh = f(hp["beta"]) * mh + f(hp["omb"]) * g
+        vh = vh - (f(hp["omb2"]) * g2) * np.sign(vh - g2)
+        new = L + ((f(1) / (np.sqrt(vh) + f(hp["tau"]))) * f(hp["eta"])) * mh
+        np.testing.assert_array_equal(mean[ci].cpu().numpy(), cur)
+        np.testing.assert_array_equal(m[ci].cpu().numpy(), mh)
+        np.testing.assert_array_equal(v[ci].cpu().numpy(), vh)
+        np.testing.assert_array_equal(out[ci].cpu().numpy(), new)
+        last.copy_(out)
+        L = new
+    del x
