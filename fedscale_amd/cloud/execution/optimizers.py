@@ -19,10 +19,45 @@ from __future__ import annotations
 from ... import kernels as kx
 from ..._native import FA_SGD_FIRST as kx_first, FA_SGD_NESTEROV as kx_nesterov
 
+_NESTEROV = kx_nesterov
+
+
+class _StepPlan:
+    """The launch tables of one (optimizer, global_model) pair, built after a general step that validated
+    every tensor: all of the optimizer's parameters had gradients and, where momentum != 0, momentum
+    buffers.  A later step re-reads only what changes between local steps — the gradients' pointers and the
+    groups' hyper-parameters — and checks by identity / pointer that nothing else moved; torch itself keeps
+    a gradient's dtype, device and size equal to its parameter's.  Anything unexpected sends the step
+    back to the general path, which rebuilds the plan."""
+
+    __slots__ = ("state", "groups", "ngroups", "group_len", "params", "pptr", "pnumel", "gidx", "has_mom", "bufs",
+                 "bptr", "glob_list", "glob_items", "glob", "globptr", "numel", "T", "stream_dev")
+
+    def __init__(self, optimizer, params, gidx, bufs, glob_list, glob):
+        import numpy as np
+
+        self.state = optimizer.state
+        self.groups = optimizer.param_groups
+        self.ngroups = len(self.groups)
+        self.group_len = [len(g['params']) for g in self.groups]
+        self.params = params
+        self.pptr = [p.data_ptr() for p in params]
+        self.pnumel = [p.numel() for p in params]
+        self.gidx = np.asarray(gidx, dtype=np.int64)
+        self.has_mom = [float(g['momentum']) != 0 for g in self.groups]
+        self.bufs = bufs
+        self.bptr = np.asarray([0 if b is None else b.data_ptr() for b in bufs], dtype=np.uint64)
+        self.glob_list, self.glob = glob_list, glob  # model order / the optimizer's parameter order
+        self.glob_items = None if glob_list is None else list(glob_list)
+        self.globptr = None if glob is None else np.asarray([t.data_ptr() for t in glob], dtype=np.uint64)
+        self.numel = np.asarray(self.pnumel, dtype=np.int64)
+        self.T = len(params)
+        self.stream_dev = params[0].device
+
 
 class ClientOptimizer(object):
     def __init__(self, sample_seed=233):
-        pass
+        self._plan = None
 
     def update_client_weight(self, conf, model, global_model=None):
         if conf.gradient_policy == 'fed-prox':
@@ -68,6 +103,78 @@ class ClientOptimizer(object):
                         return False
         return True
 
+    def _plan_step(self, optimizer, conf, global_model, fma) -> bool:
+        """The step through the cached plan; False (nothing launched) when the plan does not apply."""
+        import numpy as np
+        import torch
+
+        plan = getattr(self, "_plan", None)
+        if plan is None or optimizer.state is not plan.state or optimizer.param_groups is not plan.groups \
+                or len(plan.groups) != plan.ngroups:
+            return False
+        prox = conf.gradient_policy == 'fed-prox'
+        if prox != (plan.glob is not None):
+            return False
+        if prox:
+            if global_model is not plan.glob_list or len(global_model) != len(plan.glob_list):
+                return False
+        groups = plan.groups
+        lr, mom, damp, wd, nest = [], [], [], [], []
+        i = 0
+        for j, g in enumerate(groups):
+            m = float(g['momentum'])
+            if (m != 0) != plan.has_mom[j] or g.get('maximize', False) or g.get('differentiable', False):
+                return False
+            gp = g['params']
+            if len(gp) != plan.group_len[j]:
+                return False
+            for p in gp:  # the same parameter objects, in the same order
+                if p is not plan.params[i]:
+                    return False
+                i += 1
+            lr.append(g['lr'])
+            mom.append(m)
+            damp.append(g['dampening'])
+            wd.append(g['weight_decay'])
+            nest.append(_NESTEROV if g['nesterov'] else 0)
+        state, pptr, pnumel, bufs = plan.state, plan.pptr, plan.pnumel, plan.bufs
+        gptr = []
+        for i, p in enumerate(plan.params):
+            gr = p.grad
+            if gr is None or p.data_ptr() != pptr[i] or p.numel() != pnumel[i]:
+                return False
+            try:
+                if gr.layout is not torch.strided or not gr.is_contiguous():
+                    return False
+            except RuntimeError:
+                return False
+            gptr.append(gr.data_ptr())
+            b = bufs[i]
+            if b is not None:
+                st = state.get(p)
+                if st is None or st.get('momentum_buffer') is not b:
+                    return False
+        if prox:
+            gl = plan.glob_items
+            for i, t in enumerate(global_model):
+                if t is not gl[i]:
+                    return False
+        gi = plan.gidx
+        if plan.ngroups == 1:
+            T = plan.T
+            lr_a, mom_a = np.full(T, lr[0], np.float32), np.full(T, mom[0], np.float32)
+            damp_a, wd_a = np.full(T, damp[0], np.float64), np.full(T, wd[0], np.float32)
+            fl_a = np.full(T, nest[0], np.int32)
+        else:
+            lr_a, mom_a = np.asarray(lr, np.float32)[gi], np.asarray(mom, np.float32)[gi]
+            damp_a, wd_a = np.asarray(damp, np.float64)[gi], np.asarray(wd, np.float32)[gi]
+            fl_a = np.asarray(nest, np.int32)[gi]
+        c = float(conf.learning_rate * conf.proxy_mu) if prox else 0.0
+        kx.sgd_prox_step_groups_raw(np.asarray(pptr, np.uint64), np.asarray(gptr, np.uint64), plan.bptr,
+                                    plan.globptr, plan.numel, plan.T, lr_a, mom_a, damp_a, wd_a, fl_a, c, fma,
+                                    torch.cuda.current_stream(plan.stream_dev).cuda_stream)
+        return True
+
     def step_and_update(self, optimizer, conf, model, global_model=None, fma=True):
         """torch_client.py:236-240, ``optimizer.step()`` then ``update_client_weight(conf, model,
         global_model)``, as ONE multi-tensor launch over every parameter group (``fa_sgd_prox_step_groups``,
@@ -77,6 +184,9 @@ class ClientOptimizer(object):
         optimizer (Adam for 'nlp', maximize / differentiable SGD) takes the two reference calls."""
         import torch
 
+        if self._plan_step(optimizer, conf, global_model, fma):
+            return
+        self._plan = None
         prox = conf.gradient_policy == 'fed-prox'
         params = list(model.parameters())
         if prox and (global_model is None or len(global_model) != len(params)):
@@ -88,13 +198,16 @@ class ClientOptimizer(object):
         c = float(conf.learning_rate * conf.proxy_mu) if prox else 0.0
         # every param group in ONE launch: per-tensor lr / momentum / dampening / weight decay / flags, as
         # torch.optim.SGD keeps them per group (the detection task makes one group per parameter)
-        ps, grads, bufs, fresh, lr, mom, damp, wd, flags = [], [], [], [], [], [], [], [], []
-        for group in optimizer.param_groups:
+        ps, grads, bufs, fresh, lr, mom, damp, wd, flags, gidx = [], [], [], [], [], [], [], [], [], []
+        all_grads = True
+        for j, group in enumerate(optimizer.param_groups):
             m = float(group['momentum'])
             nest = kx_nesterov if group['nesterov'] else 0
             for p in group['params']:
                 if p.grad is None:
+                    all_grads = False
                     continue
+                gidx.append(j)
                 buf = optimizer.state[p].get('momentum_buffer') if m != 0 else None
                 first = m != 0 and buf is None
                 if first:  # enters optimizer.state only once the launch has been accepted (below)
@@ -114,7 +227,11 @@ class ClientOptimizer(object):
         for p, buf in fresh:
             optimizer.state[p]['momentum_buffer'] = buf
         stepped = {id(p) for p in ps}
+        rest = []
         if prox:  # parameters without a gradient still take the proximal step (optimizers.py:8-10)
             rest = [(p, global_model[i]) for i, p in enumerate(params) if id(p) not in stepped]
             if rest:
                 kx.prox_update([p for p, _ in rest], [g for _, g in rest], c)
+        if ps and all_grads and not rest:  # the next steps can reuse these validated tables
+            self._plan = _StepPlan(optimizer, ps, gidx, bufs, global_model if prox else None,
+                                   [gmap[id(p)] for p in ps] if prox else None)

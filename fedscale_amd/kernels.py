@@ -357,6 +357,17 @@ def sgd_prox_step_groups(params, grads, bufs, global_model, lr, momentum, dampen
          _stream(params[0]))
 
 
+def sgd_prox_step_groups_raw(pptr, gptr, bptr, globptr, numel, T: int, lr, momentum, dampening, weight_decay,
+                             flags, c: float, fma: bool, stream):
+    """fa_sgd_prox_step_groups on tables the caller has already validated (uint64 pointer arrays, int64
+    element counts, per-tensor scalar arrays of the ABI's types): the per-step launch of a plan that
+    ClientOptimizer.step_and_update checked when it built it (cloud/execution/optimizers.py)."""
+    call("fa_sgd_prox_step_groups", pptr.ctypes.data, gptr.ctypes.data, bptr.ctypes.data,
+         globptr.ctypes.data if globptr is not None else None, numel.ctypes.data, T, lr.ctypes.data,
+         momentum.ctypes.data, dampening.ctypes.data, weight_decay.ctypes.data, flags.ctypes.data, float(c),
+         int(bool(fma)), stream)
+
+
 def dp_clip_coef(params, last, max_norm: float, norm_inf: bool, coef_out: torch.Tensor):
     """coef_out[0:3] <- (total norm of param - last, clip coefficient, apply flag) (fa_dp_clip_coef)."""
     params = list(params)

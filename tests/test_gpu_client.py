@@ -405,3 +405,64 @@ def test_fused_step_falls_back_for_tensors_it_does_not_cover(gpu_device):
         ClientOptimizer().step_and_update(opt_o, conf, ours, None)
     for pr, po in zip(ref.parameters(), ours.parameters()):
         assert torch.equal(pr, po)
+
+
+def test_persistent_client_optimizer_reuses_its_step_plan(gpu_device, monkeypatch):
+    """The executor keeps one ClientOptimizer (torch_client.py:26): from the second local step on, the fused
+    step runs from its cached tables (fa_sgd_prox_step_groups on the plan's pointers) and stays bit-exact to
+    torch's SGD + FedProx through an lr schedule, a momentum change, fresh gradient tensors every step
+    (zero_grad(set_to_none=True)), a new round's global model and optimizer.load_state_dict."""
+    import argparse
+    import copy
+
+    from fedscale_amd import kernels as kx
+    from fedscale_amd.cloud.execution.optimizers import ClientOptimizer
+
+    calls = {"general": 0, "plan": 0}
+    gen, raw = kx.sgd_prox_step_groups, kx.sgd_prox_step_groups_raw
+
+    def count(kind, f):
+        def w(*a, **k):
+            calls[kind] += 1
+            return f(*a, **k)
+        return w
+
+    monkeypatch.setattr(kx, "sgd_prox_step_groups", count("general", gen))
+    monkeypatch.setattr(kx, "sgd_prox_step_groups_raw", count("plan", raw))
+    conf = argparse.Namespace(gradient_policy="fed-prox", learning_rate=0.05, proxy_mu=0.1)
+    ref, _ = _sgd_model(21, gpu_device)
+    ours = copy.deepcopy(ref)
+    kw = dict(lr=0.05, momentum=0.9, weight_decay=5e-4)
+    opt_r, opt_o = torch.optim.SGD(ref.parameters(), **kw), torch.optim.SGD(ours.parameters(), **kw)
+    sch_r = torch.optim.lr_scheduler.StepLR(opt_r, step_size=2, gamma=0.5)
+    sch_o = torch.optim.lr_scheduler.StepLR(opt_o, step_size=2, gamma=0.5)
+    co = ClientOptimizer()
+    gg = torch.Generator().manual_seed(5)
+    glob = None
+    trace = []
+    for step in range(10):
+        if step % 4 == 0:  # a new round: a new global model list (torch_client.py: one per train())
+            glob = [p.detach().clone() + 0.01 * (step + 1) for p in ref.parameters()]
+        if step == 5:  # momentum changes mid-run (still non-zero): the plan reads it per step
+            for o in (opt_r, opt_o):
+                o.param_groups[0]["momentum"] = 0.8
+        if step == 7:  # state replaced wholesale
+            opt_o.load_state_dict(copy.deepcopy(opt_r.state_dict()))
+        for pr, po in zip(ref.parameters(), ours.parameters()):
+            gr = torch.randn(pr.shape, generator=gg).to(gpu_device)
+            pr.grad, po.grad = gr.clone(), gr.clone()  # new gradient tensors every step
+        opt_r.step()
+        for idx, param in enumerate(ref.parameters()):  # optimizers.py:8-10, literally
+            param.data += conf.learning_rate * conf.proxy_mu * (param.data - glob[idx])
+        before = dict(calls)
+        co.step_and_update(opt_o, conf, ours, glob)
+        trace.append("plan" if calls["plan"] > before["plan"] else "general")
+        sch_r.step()
+        sch_o.step()
+        torch.cuda.synchronize()
+        for pr, po in zip(ref.parameters(), ours.parameters()):
+            assert torch.equal(po.detach(), pr.detach()), f"step {step}: parameter differs"
+            assert torch.equal(opt_o.state[po]["momentum_buffer"], opt_r.state[pr]["momentum_buffer"]), step
+    # general launches: step 0 (first step), 4 and 8 (new global models), 7 (state replaced); the rest from
+    # the plan
+    assert trace == ["general", "plan", "plan", "plan", "general", "plan", "plan", "general", "general", "plan"], trace
