@@ -30,25 +30,32 @@ class _StepPlan:
     a gradient's dtype, device and size equal to its parameter's.  Anything unexpected sends the step
     back to the general path, which rebuilds the plan."""
 
-    __slots__ = ("state", "groups", "ngroups", "group_len", "params", "pptr", "pnumel", "gidx", "has_mom", "bufs",
-                 "bptr", "glob_list", "glob_items", "glob", "globptr", "numel", "T", "stream_dev")
+    # Only weak references to what the executor may drop between rounds (the optimizer with its momentum
+    # buffers, the round's global model): a stale plan never keeps a model-sized buffer alive.
+    __slots__ = ("opt", "state_id", "groups_id", "ngroups", "group_len", "params", "pptr", "pnumel", "gidx",
+                 "has_mom", "bufs", "bptr", "glob_items", "glob_mptr", "globptr", "numel", "T", "stream_dev", "prox")
 
     def __init__(self, optimizer, params, gidx, bufs, glob_list, glob):
+        import weakref
+
         import numpy as np
 
-        self.state = optimizer.state
-        self.groups = optimizer.param_groups
-        self.ngroups = len(self.groups)
-        self.group_len = [len(g['params']) for g in self.groups]
-        self.params = params
+        self.opt = weakref.ref(optimizer)
+        self.state_id, self.groups_id = id(optimizer.state), id(optimizer.param_groups)
+        groups = optimizer.param_groups
+        self.ngroups = len(groups)
+        self.group_len = [len(g['params']) for g in groups]
+        self.params = [weakref.ref(p) for p in params]
         self.pptr = [p.data_ptr() for p in params]
         self.pnumel = [p.numel() for p in params]
         self.gidx = np.asarray(gidx, dtype=np.int64)
-        self.has_mom = [float(g['momentum']) != 0 for g in self.groups]
-        self.bufs = bufs
+        self.has_mom = [float(g['momentum']) != 0 for g in groups]
+        self.bufs = [None if b is None else weakref.ref(b) for b in bufs]
         self.bptr = np.asarray([0 if b is None else b.data_ptr() for b in bufs], dtype=np.uint64)
-        self.glob_list, self.glob = glob_list, glob  # model order / the optimizer's parameter order
-        self.glob_items = None if glob_list is None else list(glob_list)
+        self.prox = glob_list is not None
+        # the global model's tensors (model order), weakly; their pointers in the optimizer's order
+        self.glob_items = None if glob_list is None else [weakref.ref(t) for t in glob_list]
+        self.glob_mptr = None if glob_list is None else [t.data_ptr() for t in glob_list]
         self.globptr = None if glob is None else np.asarray([t.data_ptr() for t in glob], dtype=np.uint64)
         self.numel = np.asarray(self.pnumel, dtype=np.int64)
         self.T = len(params)
@@ -109,16 +116,15 @@ class ClientOptimizer(object):
         import torch
 
         plan = getattr(self, "_plan", None)
-        if plan is None or optimizer.state is not plan.state or optimizer.param_groups is not plan.groups \
-                or len(plan.groups) != plan.ngroups:
+        if plan is None or plan.opt() is not optimizer or id(optimizer.state) != plan.state_id \
+                or id(optimizer.param_groups) != plan.groups_id or len(optimizer.param_groups) != plan.ngroups:
             return False
         prox = conf.gradient_policy == 'fed-prox'
-        if prox != (plan.glob is not None):
+        if prox != plan.prox:
             return False
-        if prox:
-            if global_model is not plan.glob_list or len(global_model) != len(plan.glob_list):
-                return False
-        groups = plan.groups
+        if prox and (global_model is None or len(global_model) != len(plan.glob_items)):
+            return False
+        groups = optimizer.param_groups
         lr, mom, damp, wd, nest = [], [], [], [], []
         i = 0
         for j, g in enumerate(groups):
@@ -129,7 +135,7 @@ class ClientOptimizer(object):
             if len(gp) != plan.group_len[j]:
                 return False
             for p in gp:  # the same parameter objects, in the same order
-                if p is not plan.params[i]:
+                if p is not plan.params[i]():
                     return False
                 i += 1
             lr.append(g['lr'])
@@ -137,9 +143,10 @@ class ClientOptimizer(object):
             damp.append(g['dampening'])
             wd.append(g['weight_decay'])
             nest.append(_NESTEROV if g['nesterov'] else 0)
-        state, pptr, pnumel, bufs = plan.state, plan.pptr, plan.pnumel, plan.bufs
+        state, pptr, pnumel, bufs = optimizer.state, plan.pptr, plan.pnumel, plan.bufs
         gptr = []
-        for i, p in enumerate(plan.params):
+        for i, pr in enumerate(plan.params):
+            p = pr()
             gr = p.grad
             if gr is None or p.data_ptr() != pptr[i] or p.numel() != pnumel[i]:
                 return False
@@ -151,13 +158,13 @@ class ClientOptimizer(object):
             gptr.append(gr.data_ptr())
             b = bufs[i]
             if b is not None:
-                st = state.get(p)
-                if st is None or st.get('momentum_buffer') is not b:
+                buf, st = b(), state.get(p)
+                if buf is None or st is None or st.get('momentum_buffer') is not buf:
                     return False
-        if prox:
-            gl = plan.glob_items
+        if prox:  # the same global tensors (a new round hands a new list: the general path rebuilds)
+            gl, gp = plan.glob_items, plan.glob_mptr
             for i, t in enumerate(global_model):
-                if t is not gl[i]:
+                if t is not gl[i]() or t.data_ptr() != gp[i]:
                     return False
         gi = plan.gidx
         if plan.ngroups == 1:
