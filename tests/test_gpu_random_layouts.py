@@ -95,3 +95,54 @@ def test_random_layout_round_matches_oracle(gpu_device, seed):
             assert_state_close(got, want, 1e-6, ctx)
         else:
             assert_state_close(got, want, 1e-5, ctx, int_slack=1)
+
+
+@pytest.mark.parametrize("seed", range(32))
+def test_random_layout_sharded_matches_oracle(gpu_device, seed):
+    """The same random rounds through a ShardedModelAdapter of 2-4 parts on the one card (copy transport):
+    the parts' slices fall anywhere, across tensors and through 0-d / empty entries."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator, DeviceAsyncAggregator
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+    from fedscale_amd.cloud.internal.sharded_model_adapter import ShardedModelAdapter
+    from oracle.cpu_reference import OracleAggregator, OracleModel, OracleModelAdapter, OracleServerOptimizer
+
+    rng = np.random.default_rng(5000 + seed)
+    policy = POLICIES[seed % len(POLICIES)]
+    names, tensors = _layout(rng)
+    a = dict(DEFAULT_ARGS)
+    a["gradient_policy"] = policy if policy in ("fed-yogi", "q-fedavg") else None
+    a["qfed_q"] = float(rng.choice([0.0, 1.0, 2.0]))
+    args, oargs = argparse.Namespace(**a), argparse.Namespace(**a)
+    n = int(rng.integers(2, 5))
+    cap = [None, 1, 3][int(rng.integers(0, 3))]
+    mode = a["gradient_policy"]
+    adapter = ShardedModelAdapter(StateDictModule(names, tensors), optimizer=TorchServerOptimizer(mode, args, "cuda:0"),
+                                  devices=[0] * n, transport="copy", staging_capacity=cap)
+    oracle = OracleAggregator(OracleModelAdapter(OracleModel(names, tensors), OracleServerOptimizer(mode, oargs)),
+                              oargs, asynchronous=policy == "fedbuff")
+    agg = DeviceAsyncAggregator(adapter, args) if policy == "fedbuff" else DeviceAggregator(adapter, args)
+    for r in range(2):
+        K = int(rng.integers(1, 17))
+        ups = _uploads(rng, names, tensors, K, as_list_every=int(rng.integers(0, 3)))
+        if policy == "fedbuff":
+            for o in (agg, oracle):
+                o.round = 3 + r
+            for res in ups:
+                v = 3 + r - int(rng.integers(0, 6))
+                agg.client_task_model_version[res["client_id"]] = v
+                oracle.client_task_model_version[res["client_id"]] = v
+        agg.start_round(K)
+        oracle.start_round(K)
+        for res in ups:
+            oracle.on_result({**res, "update_weight": res["update_weight"]})
+            agg.on_result(res)
+        got = adapter.get_weights()
+        want = [t.numpy() for t in oracle.model_wrapper.get_weights()]
+        ctx = f"seed {seed} {policy} parts={n} r{r} K={K} cap={cap}"
+        if policy in ("fedavg", "fedbuff"):
+            assert_state_equal(got, want, ctx)
+            assert_state_equal(list(agg.model_weights), [np.asarray(w) for w in oracle.model_weights], ctx + " mean")
+        elif policy == "fed-yogi":
+            assert_state_close(got, want, 1e-6, ctx)
+        else:
+            assert_state_close(got, want, 1e-5, ctx, int_slack=1)
