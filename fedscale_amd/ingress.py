@@ -67,6 +67,9 @@ class _Unpickler(pickle.Unpickler):
         return super().find_class(module, name)
 
 
+_LEAVES = frozenset((str, int, float, bool, bytes, type(None), complex))
+
+
 class _Fallback(Exception):
     pass
 
@@ -115,26 +118,34 @@ class _Materializer:
         t = type(obj)
         if t is _ArrayStub:
             return self.array(obj)
-        if t is dict:
+        if t is dict:  # (the upload's name -> array dict: leaves handled inline, no call per array)
             for k, v in obj.items():
                 if type(k) is _ArrayStub:
                     raise _Fallback("array used as a key")
-                nv = self.walk(v, depth + 1)
-                if nv is not v:
-                    obj[k] = nv
+                tv = type(v)
+                if tv is _ArrayStub:
+                    obj[k] = self.array(v)
+                elif tv not in _LEAVES:
+                    nv = self.walk(v, depth + 1)
+                    if nv is not v:
+                        obj[k] = nv
             return obj
         if t is list:
             for i, v in enumerate(obj):
-                nv = self.walk(v, depth + 1)
-                if nv is not v:
-                    obj[i] = nv
+                tv = type(v)
+                if tv is _ArrayStub:
+                    obj[i] = self.array(v)
+                elif tv not in _LEAVES:
+                    nv = self.walk(v, depth + 1)
+                    if nv is not v:
+                        obj[i] = nv
             return obj
         if t is tuple:
             items = [self.walk(v, depth + 1) for v in obj]
             if any(a is not b for a, b in zip(items, obj)):
                 return tuple(items)
             return obj
-        if t in (str, int, float, bool, bytes, type(None), complex):
+        if t in _LEAVES:
             return obj
         if isinstance(obj, (np.generic, np.ndarray)):
             return obj
