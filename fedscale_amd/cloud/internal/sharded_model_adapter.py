@@ -108,6 +108,8 @@ class ShardedModelAdapter(TorchModelAdapter):
     # ---- rounds -----------------------------------------------------------------------------------
     def begin_round(self, K: int, policy: str, capacity: Optional[int] = None, keep_mean=True) -> ShardedRound:
         cap = capacity or self.staging_capacity
+        if not cap and all(p.staging is not None and p.staging.capacity >= K for p in self.parts):
+            cap = K  # the round fits the staging every part already holds (no free-memory query)
         if not cap:  # one capacity for all parts, so they fold their chunks in step; parts sharing a
             # device share its budget (half of the free HBM)
             per_dev = {}
