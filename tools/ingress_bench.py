@@ -4,7 +4,7 @@ torch_client.py:76-78), pass through DeviceAggregator.update_weight_aggregation 
 memory -> async H2D -> chunked in-order reduction), and the round ends with get_weights() (D2H egress,
 torch_model_adapter.py:41-47).
 
-usage: python tools/ingress_bench.py [K] [rounds] [layout=resnet18|femnist] [pack_workers,...]
+usage: python tools/ingress_bench.py [K] [rounds] [layout=resnet18|femnist|p25m] [pack_workers,...]
 """
 import json
 import os
@@ -40,12 +40,26 @@ def main():
     json.dump(allout, open(os.path.join(ROOT, "gpurun_out", f"ingress_{which}_k{K}.json"), "w"), indent=1)
 
 
+def _layout(which):
+    """resnet18 (config 3), femnist (config 1) or p25m: the headline's 25 M fp32 parameters as 10 tensors
+    of 2.5 M (a 100 MB update)."""
+    import torch
+
+    from fedscale_amd import synth
+
+    if which == "resnet18":
+        return synth.resnet18_layout()
+    if which == "p25m":
+        return [f"l{i}.weight" for i in range(10)], [(2500, 1000)] * 10, [torch.float32] * 10
+    return synth.femnist_cnn_layout()
+
+
 def run(K, rounds, which, workers, loader=None, async_ingress=False):
     from fedscale_amd import synth
     from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
     from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
 
-    names, shapes, dtypes = synth.resnet18_layout() if which == "resnet18" else synth.femnist_cnn_layout()
+    names, shapes, dtypes = _layout(which)
     model = synth.LayoutModule(names, shapes, dtypes)
     adapter = TorchModelAdapter(model, device="cuda:0")
     if workers or async_ingress:
@@ -134,7 +148,7 @@ def egress(which, requests=8):
     from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
     from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
 
-    names, shapes, dtypes = synth.resnet18_layout() if which == "resnet18" else synth.femnist_cnn_layout()
+    names, shapes, dtypes = _layout(which)
     model = synth.LayoutModule(names, shapes, dtypes)
     adapter = TorchModelAdapter(model, device="cuda:0")
     agg = DeviceAggregator(adapter)
