@@ -603,21 +603,38 @@ __device__ __forceinline__ float fast_div(float a, float b, float r) {
 #ifndef QF_INFCHK
 #define QF_INFCHK 1
 #endif
+// QF_EMAX 0: the upper bound is tested on max |a| alone (|a| < 2^80 also excludes +-inf), so the frexp
+// exponent feeds only the lower bound — one max3 per two elements fewer.  1: round 1's form.
+#ifndef QF_EMAX
+#define QF_EMAX 1
+#endif
+// QF_PART: squares per fp32 partial before the fp64 sum (4, 8 or 16; each partial is one cvt + one fp64 add)
+#ifndef QF_PART
+#define QF_PART 4
+#endif
+static_assert(QF_PART == 4 || QF_PART == 8 || QF_PART == 16, "QF_PART: 4, 8 or 16");
 struct DivRange {
-  int emin = 0, emax = 0;  // frexp exponents (0 for +-0): |a| in [2^(e-1), 2^e)
-#if QF_INFCHK == 1
+  int emin = 0;  // frexp exponents (0 for +-0): |a| in [2^(e-1), 2^e)
+#if QF_EMAX
+  int emax = 0;
+#endif
+#if QF_INFCHK == 1 || !QF_EMAX
   float amax = 0.f;        // catches +-inf (frexp reports 0 for it)
 #endif
   __device__ __forceinline__ void add(float a) {
     const int e = __builtin_amdgcn_frexp_expf(a);
     emin = e < emin ? e : emin;
+#if QF_EMAX
     emax = e > emax ? e : emax;
-#if QF_INFCHK == 1
+#endif
+#if QF_INFCHK == 1 || !QF_EMAX
     amax = __builtin_fmaxf(amax, __builtin_fabsf(a));
 #endif
   }
   __device__ __forceinline__ bool ok() const {
-#if QF_INFCHK == 1
+#if !QF_EMAX
+    return emin >= -79 && amax < 0x1p80f;
+#elif QF_INFCHK == 1
     return emin >= -79 && emax <= 80 && amax < __builtin_inff();
 #else
     return emin >= -79 && emax <= 80;
@@ -711,9 +728,15 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       }
       double acc = 0.0;
 #pragma unroll
-      for (int j = 0; j < QF_V; ++j) {
-        const f4 g2 = g[j] * g[j];  // torch.square(grad), fp32
-        acc += (double)((g2.x + g2.y) + (g2.z + g2.w));  // 4-term fp32 partial, then fp64
+      for (int j = 0; j < QF_V; j += QF_PART / 4) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < QF_PART / 4; ++i) {
+          const f4 g2 = g[j + i] * g[j + i];  // torch.square(grad), fp32
+          const float s4 = (g2.x + g2.y) + (g2.z + g2.w);
+          s = i == 0 ? s4 : s + s4;
+        }
+        acc += (double)s;  // QF_PART-term fp32 partial, then fp64
       }
 #if QF_INFCHK == 1
       const bool fast_ok = rng.ok();
@@ -728,8 +751,17 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
           g[j].y = __fdiv_rn(t[j].y, q.lr);
           g[j].z = __fdiv_rn(t[j].z, q.lr);
           g[j].w = __fdiv_rn(t[j].w, q.lr);
-          const f4 g2 = g[j] * g[j];
-          acc += (double)((g2.x + g2.y) + (g2.z + g2.w));
+        }
+#pragma unroll
+        for (int j = 0; j < QF_V; j += QF_PART / 4) {  // the same partials as the fast path
+          float s = 0.f;
+#pragma unroll
+          for (int i = 0; i < QF_PART / 4; ++i) {
+            const f4 g2 = g[j + i] * g[j + i];
+            const float s4 = (g2.x + g2.y) + (g2.z + g2.w);
+            s = i == 0 ? s4 : s + s4;
+          }
+          acc += (double)s;
         }
       }
 #pragma unroll

@@ -44,6 +44,7 @@ def main():
     ws = torch.empty(max(w for _, _, w in libs.values()) // 8 + 1, dtype=torch.float64, device="cuda")
     st = torch.cuda.current_stream().cuda_stream
     times = {n: [] for n in libs}
+    rels = {}
     ref = ref_chain = ref_sq = None
     for r in range(rounds):
         for n, (f, use_chain, _) in libs.items():
@@ -57,7 +58,9 @@ def main():
             else:
                 assert torch.equal(delta, ref), f"{n}: delta differs"
                 rel = ((sq - ref_sq).abs() / ref_sq).max().item()
-                assert rel < 1e-12, f"{n}: sqnorm differs by {rel}"
+                # variants with another fp32 partial length (QF_PART, _p*) round the norms differently
+                assert rel < 1e-8, f"{n}: sqnorm differs by {rel}"
+                rels[n] = max(rels.get(n, 0.0), rel)
             if use_chain:
                 if ref_chain is None:
                     ref_chain = chain.clone()
@@ -79,7 +82,7 @@ def main():
     b = 4 * K * P + 8 * P + 8 * K
     print(f"--- K={K} P={P} (GB/s over 4KP + 8P + 8K; +chain moves 4P more)")
     for n, t in sorted(times.items(), key=lambda kv: np.median(kv[1])):
-        print(f"{n:40s} {np.median(t):8.3f} ms {b / (np.median(t) * 1e-3) / 1e9:8.1f} GB/s", flush=True)
+        print(f"{n:40s} {np.median(t):8.3f} ms {b / (np.median(t) * 1e-3) / 1e9:8.1f} GB/s  sqnorm rel {rels.get(n, 0.0):.1e}", flush=True)
 
 
 if __name__ == "__main__":
