@@ -1135,6 +1135,10 @@ extern "C" int64_t fa_qfed_workspace_bytes(int32_t K) {  // enough for either ke
 #ifndef QF_PLAIN_GLDS
 #define QF_PLAIN_GLDS 0
 #endif
+#ifndef QF_WIDE_BYTES
+#define QF_WIDE_BYTES (1LL << 31)  // largest QF_G-row span served by one descriptor (tuning knob; <= 2^31)
+#endif
+static_assert(QF_WIDE_BYTES <= (1LL << 31), "QF_WIDE_BYTES: the rows plus the OOB sentinel must stay below 2^32");
 
 static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const float* last, const float* alpha,
                         float lr, int fast, float* delta, float* chain, double* sqnorm, void* workspace,
@@ -1145,7 +1149,7 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
   q.fast = fast;
   // WIDE needs QF_G rows plus the sentinel below 2^32; otherwise per-row descriptors over column
   // windows of 2^28 floats (1 GiB), one launch each; the gathers add their partial norms in order.
-  const bool wide = (int64_t)ld * 4 * QF_G <= (1LL << 31);
+  const bool wide = (int64_t)ld * 4 * QF_G <= QF_WIDE_BYTES;
   const int64_t win = wide ? (P > 0 ? P : 1) : (1LL << 28);
   for (int64_t w0 = 0; w0 < P || w0 == 0; w0 += win) {
     QfArgs qw = q;
