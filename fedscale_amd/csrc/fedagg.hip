@@ -17,6 +17,7 @@
 #include <stdint.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <unistd.h>
@@ -1773,6 +1774,38 @@ struct GatherPool {
 std::mutex g_pool_mu;
 GatherPool* g_pool = nullptr;
 pid_t g_pool_pid = 0;  // a forked child inherits the pointer but not the threads: rebuild there
+
+// Pieces of >= 64 KiB are written with non-temporal (streaming) stores: the pinned row is read next by
+// the H2D copy engine, not by this core, and a cached store first reads the line it overwrites
+// (read-for-ownership), so a plain memcpy moves 3 bytes of host DRAM traffic per byte copied where this
+// moves 2.  Source loads stay cached (they are read once either way).  FEDAGG_GATHER_NT=0 turns it off.
+bool gather_nt() {
+  static const bool on = [] {
+    const char* e = getenv("FEDAGG_GATHER_NT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+void copy_piece(char* d, const char* s, size_t n) {
+  if (n < (64u << 10) || !gather_nt()) {
+    memcpy(d, s, n);
+    return;
+  }
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  const size_t head = (64 - ((uintptr_t)d & 63)) & 63;  // align the destination to a cache line
+  memcpy(d, s, head);
+  d += head, s += head, n -= head;
+  const size_t lines = n / 64;
+  for (size_t i = 0; i < lines; ++i, d += 64, s += 64) {
+    v4 a, b, c, e;
+    memcpy(&a, s, 16), memcpy(&b, s + 16, 16), memcpy(&c, s + 32, 16), memcpy(&e, s + 48, 16);
+    __builtin_nontemporal_store(a, reinterpret_cast<v4*>(d));
+    __builtin_nontemporal_store(b, reinterpret_cast<v4*>(d + 16));
+    __builtin_nontemporal_store(c, reinterpret_cast<v4*>(d + 32));
+    __builtin_nontemporal_store(e, reinterpret_cast<v4*>(d + 48));
+  }
+  memcpy(d, s, n - lines * 64);
+}
 }  // namespace
 
 extern "C" int fa_host_gather(void* dst, const void* const* srcs, const int64_t* dst_off, const int64_t* nbytes,
@@ -1785,7 +1818,8 @@ extern "C" int fa_host_gather(void* dst, const void* const* srcs, const int64_t*
   }
   char* d = static_cast<char*>(dst);
   if (threads <= 1 || total < (4 << 20)) {
-    for (int i = 0; i < n; ++i) memcpy(d + dst_off[i], srcs[i], (size_t)nbytes[i]);
+    for (int i = 0; i < n; ++i) copy_piece(d + dst_off[i], static_cast<const char*>(srcs[i]), (size_t)nbytes[i]);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
     return FA_OK;
   }
   if (threads > 64) threads = 64;
@@ -1810,8 +1844,10 @@ extern "C" int fa_host_gather(void* dst, const void* const* srcs, const int64_t*
       const int64_t a = pos, b = pos + nbytes[i];
       pos = b;
       const int64_t s0 = a > lo ? a : lo, s1 = b < hi ? b : hi;
-      if (s0 < s1) memcpy(d + dst_off[i] + (s0 - a), static_cast<const char*>(srcs[i]) + (s0 - a), (size_t)(s1 - s0));
+      if (s0 < s1) copy_piece(d + dst_off[i] + (s0 - a), static_cast<const char*>(srcs[i]) + (s0 - a), (size_t)(s1 - s0));
     }
+    // order the streaming stores before the pool reports done (the caller's H2D reads the row next)
+    std::atomic_thread_fence(std::memory_order_seq_cst);
   });
   return FA_OK;
 }

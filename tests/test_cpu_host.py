@@ -151,3 +151,31 @@ def test_native_host_gather(workers):
     lay.pack_host(vals, f, np.zeros(1, np.int64), workers=workers)
     np.testing.assert_array_equal(f[:lay.P], np.concatenate([v.reshape(-1) for v in vals]))
     assert np.all(f[lay.P:] == -1)
+
+
+@pytest.mark.parametrize("workers", [1, 3, 16])
+def test_native_host_gather_streaming_copy_odd_offsets(workers):
+    """The streaming-store copy of large pieces (>= 64 KiB): byte-exact at destination and source offsets
+    off every alignment, with tails shorter than a cache line, and nothing written outside the pieces."""
+    from fedscale_amd import _native
+
+    rng = np.random.default_rng(10 + workers)
+    sizes = [65536, 65537 + 13, 3, 1 << 20, 200_001, 64 * 1024 + 63, 5_000_000]
+    src_buf = rng.integers(0, 256, size=sum(sizes) + 64 * len(sizes), dtype=np.uint8)
+    srcs, offs, pos, s_at = [], [], 7, 1
+    for n in sizes:
+        srcs.append(src_buf.ctypes.data + s_at)
+        offs.append(pos)
+        s_at += n + 5
+        pos += n + 3  # gaps of 3 bytes stay untouched
+    dst = np.full(pos + 64, 0xAB, dtype=np.uint8)
+    ps = np.asarray(srcs, dtype=np.uint64)
+    po = np.asarray(offs, dtype=np.int64)
+    pn = np.asarray(sizes, dtype=np.int64)
+    _native.call("fa_host_gather", dst.ctypes.data, ps.ctypes.data, po.ctypes.data, pn.ctypes.data, len(sizes), workers)
+    want = np.full_like(dst, 0xAB)
+    s_at = 1
+    for o, n in zip(offs, sizes):
+        want[o:o + n] = src_buf[s_at:s_at + n]
+        s_at += n + 5
+    np.testing.assert_array_equal(dst, want)
