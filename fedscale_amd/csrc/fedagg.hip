@@ -1557,6 +1557,9 @@ __device__ __forceinline__ void hb_add(float& acc, int& cnt, float v, bool hit) 
 #ifndef HB_FLAT_U
 #define HB_FLAT_U 1
 #endif
+#ifndef HB_DPREFETCH
+#define HB_DPREFETCH 0  // 1: measured 2 % slower (profiles/r02_tune_heterofl_dprefetch.log)
+#endif
 __device__ __forceinline__ void prefix_box_flat(const float* __restrict__ xs, const int64_t* __restrict__ dk,
                                                 int64_t dstride, int K, int64_t goff, int64_t RL, int64_t n,
                                                 int64_t c0, float* glob) {
@@ -1578,20 +1581,35 @@ __device__ __forceinline__ void prefix_box_flat(const float* __restrict__ xs, co
       acc[j][i] = 0.f;  // tmp_v = v.new_zeros(..., dtype=torch.float32)
       cnt[j][i] = 0;
     }
+  // the clients' box descriptors are scalar loads; HB_DPREFETCH requests the next group's while this
+  // group's vector loads are in flight
+  int64_t dsc[HB_FLAT_U][4];
+  auto desc_of = [&](int m, int64_t(&v)[4]) {
+    const bool mv = m < K;
+    const int64_t* d = dk + (int64_t)(mv ? m : 0) * dstride;
+    v[0] = d[0], v[1] = mv ? d[1] : 0, v[2] = d[2], v[3] = d[3];
+  };
+#pragma unroll
+  for (int u = 0; u < HB_FLAT_U; ++u) desc_of(u, dsc[u]);
   for (int m0 = 0; m0 < K; m0 += HB_FLAT_U) {
     f4 t[HB_FLAT_U][HB_FLAT_J];
     int64_t len[HB_FLAT_U][HB_FLAT_J];
 #pragma unroll
     for (int u = 0; u < HB_FLAT_U; ++u) {
-      const bool mv = m0 + u < K;
-      const int64_t* d = dk + (int64_t)(mv ? m0 + u : 0) * dstride;
-      const int64_t off = d[0], om = mv ? d[1] : 0, Lm = d[2], ldm = d[3];
+#if !HB_DPREFETCH
+      desc_of(m0 + u, dsc[u]);
+#endif
+      const int64_t off = dsc[u][0], om = dsc[u][1], Lm = dsc[u][2], ldm = dsc[u][3];
 #pragma unroll
       for (int j = 0; j < HB_FLAT_J; ++j) {
         len[u][j] = (in[j] && o[j] < om) ? Lm : 0;  // covered columns of this row: [0, L_m)
         t[u][j] = r[j] < len[u][j] ? hb_load(xs + off + o[j] * ldm + r[j]) : f4{0.f, 0.f, 0.f, 0.f};
       }
     }
+#if HB_DPREFETCH
+#pragma unroll
+    for (int u = 0; u < HB_FLAT_U; ++u) desc_of(m0 + HB_FLAT_U + u, dsc[u]);
+#endif
 #pragma unroll
     for (int u = 0; u < HB_FLAT_U; ++u)
 #pragma unroll
