@@ -51,6 +51,34 @@ def test_c3_resnet18_layout_fedavg_k1000(gpu_device):
     del x
 
 
+def test_headline_fedavg_and_fedbuff_k1000_p25m(gpu_device):
+    """The bench headline's exact launch (1000 x 25M fp32, FedAvg mean, the capped-grid V=32 variant) and
+    FedBuff's weighted form of it (aggregator.py:497-507, async_aggregator.py:115-137), column-sampled."""
+    from fedscale_amd import kernels as kx
+    from fedscale_amd import synth
+    from fedscale_amd.bucket import round_up
+
+    K, P, seed = 1000, 25_000_000, 2024
+    ld = round_up(P, 64)
+    x = torch.empty(K, ld, device="cuda")
+    synth.fill(x, K, P, seed=seed)
+    out = torch.empty(ld, device="cuda")
+    cols = _sample_cols(P, n=2048, seed=2)
+    ci = torch.from_numpy(cols).cuda()
+    kx.reduce(x, K, P, out, denom=float(np.float32(K)), finalize=True)
+    np.testing.assert_array_equal(out[ci].cpu().numpy(), np.divide(_host_seq_sum(seed, K, cols), K))
+    # FedBuff: staleness weights 1/sqrt(1 + s_k), s_k = k mod 6 (SURVEY §8d), fp32 products added in order
+    w = np.asarray([1 / (1 + (k % 6)) ** 0.5 for k in range(K)], dtype=np.float32)
+    denom = np.float32(np.sum(w.astype(np.float64)))
+    kx.reduce(x, K, P, out, a=torch.from_numpy(w).cuda(), denom=float(denom), finalize=True)
+    acc = np.zeros(len(cols), np.float32)
+    for c0 in range(0, K, 100):
+        for k, row in zip(range(c0, c0 + 100), synth.host_columns(seed, range(c0, c0 + 100), cols)):
+            acc = acc + w[k] * row
+    np.testing.assert_array_equal(out[ci].cpu().numpy(), np.divide(acc, denom))
+    del x
+
+
 def test_c4_fedyogi_k1000_p25m(gpu_device):
     """Config 4 (per-GPU shard): fused reduce + FedYoGi over 1000 x 25M, two rounds of state."""
     from fedscale_amd import kernels as kx

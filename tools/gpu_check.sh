@@ -67,7 +67,7 @@ fi
 if [[ $STAGE == dist ]]; then
   timeout -k 10 900 python -m pytest tests/test_distributed.py -m gpu -x -q > $OUT/pytest_dist.log 2>&1 || { tail -40 $OUT/pytest_dist.log; exit 1; }
   tail -3 $OUT/pytest_dist.log
-  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 1 --clients 100 --params 4000000 --dist-backend gloo --reassemble > $OUT/bench_dist2.log 2>&1 || { tail -30 $OUT/bench_dist2.log; exit 1; }
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 1 --clients 100 --params 4000000 --dist-backend gloo --mem-fraction 0.3 > $OUT/bench_dist2.log 2>&1 || { tail -30 $OUT/bench_dist2.log; exit 1; }
   grep '^{' $OUT/bench_dist2.log
   for pol in fedavg fedyogi qfedavg; do
     timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 5 --warmup 1 --clients 100 --params 4000000 --dist-backend gloo --shard clients --policy $pol > $OUT/bench_dist2_clients_$pol.log 2>&1 || { tail -30 $OUT/bench_dist2_clients_$pol.log; exit 1; }
