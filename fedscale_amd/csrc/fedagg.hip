@@ -364,6 +364,10 @@ static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_w
 #ifndef FA_BAL_SHORT_K
 #define FA_BAL_SHORT_K 200  // rounds of fewer clients: one round over every CU when the tiles fit
 #endif
+#ifndef FA_CAP_SW_MAX
+#define FA_CAP_SW_MAX 32  // widest tile (strips per wave) of the multi-round capped plan (tuning knob, 8..32)
+#endif
+static_assert(FA_CAP_SW_MAX >= 8 && FA_CAP_SW_MAX <= 32, "FA_CAP_SW_MAX: 8..32");
 template <int V, int U, int EPI, bool W>
 static void launch_balanced(RedArgs r, int64_t sw, int64_t rounds, hipStream_t st) {
   const int64_t S = (r.P4 + 63) / 64;
@@ -402,11 +406,14 @@ static void launch_plan(const RedArgs& r, hipStream_t st) {
     const int64_t S = (r.P4 + 63) / 64;
     const int64_t g1 = r.K < FA_BAL_SHORT_K ? (int64_t)cu_count() : cap;  // short rounds: one round, all CUs
     const int64_t sw1 = (S + (int64_t)FA_RED_WAVES * g1 - 1) / ((int64_t)FA_RED_WAVES * g1);
-    if (sw1 > 32) {  // R rounds of the capped grid
-      const int64_t per_round = (int64_t)FA_RED_WAVES * 32 * cap;
+    if (sw1 > 32) {  // R rounds of the capped grid, tiles at most FA_CAP_SW_MAX strips wide
+      const int64_t per_round = (int64_t)FA_RED_WAVES * FA_CAP_SW_MAX * cap;
       const int64_t R = (S + per_round - 1) / per_round;
       const int64_t sw = (S + (int64_t)FA_RED_WAVES * R * cap - 1) / ((int64_t)FA_RED_WAVES * R * cap);
-      launch_balanced<32, 1, EPI, W>(r, sw, R, st);
+      if (sw > 16)
+        launch_balanced<32, 1, EPI, W>(r, sw, R, st);
+      else
+        launch_balanced<16, 2, EPI, W>(r, sw, R, st);
       return;
     }
     if (sw1 >= 8) {  // one round of wide tiles on (about) the capped grid
