@@ -567,6 +567,13 @@ def main():
         reassembly_ms = _max_over_ranks([(time.perf_counter() - t0r) * 1e3 / 5], dev, world, args.dist_backend)[0]
     alg_bytes = w.alg_bytes
     P_local, n_passes = w.P, len(w.passes)
+    # launches of the dominant kernel per step: fa_reduce runs long buckets as column windows (fedagg.hip
+    # FA_WINDOWS), so the per-launch figures rocprof reports are the step's divided by this
+    from fedscale_amd import kernels as kx
+    if policy == "qfedavg":
+        launches = n_passes
+    else:
+        launches = n_passes * kx.reduce_launches(w.C if n_passes > 1 else K, P_local, weighted=policy == "fedbuff")
     w.free()
     del w
 
@@ -627,7 +634,8 @@ def main():
                                     {"fedavg": "k_reduce (fa_reduce FA_FINALIZE)",
                                      "fedbuff": "k_reduce weighted (fa_reduce FA_FINALIZE)",
                                      "fedyogi": "k_reduce EPI_YOGI (fa_reduce_yogi)"}[policy]),
-                         "alg_bytes_per_launch": alg_bytes},
+                         "alg_bytes_per_launch": alg_bytes / launches, "launches_per_step": launches,
+                         "kernel_ms_per_launch": kern_ms / launches},
         }
         if reassembly_ms is not None:
             res["reassembly_ms"] = reassembly_ms

@@ -306,6 +306,17 @@ static int resident_blocks() {
   return cache[dev];
 }
 
+// fa_reduce_launches() runs the launch plan with g_plan_count set: every k_reduce launch site then counts
+// instead of launching, so the plan has one source of truth.
+static thread_local int64_t* g_plan_count = nullptr;
+#define FA_RED_LAUNCH(kern, grid, block, st, args)         \
+  do {                                                     \
+    if (g_plan_count)                                      \
+      ++*g_plan_count;                                     \
+    else                                                   \
+      hipLaunchKernelGGL(kern, grid, block, 0, st, args);  \
+  } while (0)
+
 // launch variant (V, U) over float4 columns [col, col_end); `full_waves_only` keeps only whole waves of
 // workgroups (a last partial wave is kept when it would still occupy >= 90 % of the resident slots: a
 // narrower variant is ~6 % slower per byte, so handing such a wave down costs more than its idle 10 %)
@@ -330,9 +341,9 @@ static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_w
   if (cap > 0 && nblk > cap) {
     const int64_t rounds = (nblk + cap - 1) / cap;
     const int64_t grid = (nblk + rounds - 1) / rounds;
-    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, true>), dim3((unsigned)grid), dim3(64 * FA_RED_WAVES), 0, st, r);
+    FA_RED_LAUNCH((k_reduce<V, U, EPI, W, true>), dim3((unsigned)grid), dim3(64 * FA_RED_WAVES), st, r);
   } else {
-    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, false>), dim3((unsigned)nblk), dim3(64 * FA_RED_WAVES), 0, st, r);
+    FA_RED_LAUNCH((k_reduce<V, U, EPI, W, false>), dim3((unsigned)nblk), dim3(64 * FA_RED_WAVES), st, r);
   }
   const int64_t end = col + nblk * span;
   return (full_waves_only && end < col_end) ? end : col_end;
@@ -378,16 +389,44 @@ static void launch_balanced(RedArgs r, int64_t sw, int64_t rounds, hipStream_t s
   const dim3 blk(64 * FA_RED_WAVES);
   if (grid < r.ntiles) {
     if (sw == V)
-      hipLaunchKernelGGL((k_reduce<V, U, EPI, W, true, true>), dim3((unsigned)grid), blk, 0, st, r);
+      FA_RED_LAUNCH((k_reduce<V, U, EPI, W, true, true>), dim3((unsigned)grid), blk, st, r);
     else
-      hipLaunchKernelGGL((k_reduce<V, U, EPI, W, true, false>), dim3((unsigned)grid), blk, 0, st, r);
+      FA_RED_LAUNCH((k_reduce<V, U, EPI, W, true, false>), dim3((unsigned)grid), blk, st, r);
   } else if (sw == V) {
-    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, false, true>), dim3((unsigned)r.ntiles), blk, 0, st, r);
+    FA_RED_LAUNCH((k_reduce<V, U, EPI, W, false, true>), dim3((unsigned)r.ntiles), blk, st, r);
   } else {
-    hipLaunchKernelGGL((k_reduce<V, U, EPI, W, false, false>), dim3((unsigned)r.ntiles), blk, 0, st, r);
+    FA_RED_LAUNCH((k_reduce<V, U, EPI, W, false, false>), dim3((unsigned)r.ntiles), blk, st, r);
   }
 }
 
+// One round of tiles over the column window [s0, s0 + ns) strips (64 float4 columns each) on about `cap`
+// workgroups: the kernel's col0 / P4 bound the window, outputs stay indexed by absolute column.
+template <int EPI, bool W>
+static void launch_window(RedArgs r, int64_t s0, int64_t ns, int64_t cap, hipStream_t st) {
+  const int64_t sw = (ns + (int64_t)FA_RED_WAVES * cap - 1) / ((int64_t)FA_RED_WAVES * cap);
+  r.col0 = s0 * 64;
+  r.P4 = (s0 + ns) * 64 < r.P4 ? (s0 + ns) * 64 : r.P4;
+  r.sw = (int)sw;
+  r.ntiles = (ns + (int64_t)FA_RED_WAVES * sw - 1) / ((int64_t)FA_RED_WAVES * sw);
+  const dim3 grid((unsigned)r.ntiles), blk(64 * FA_RED_WAVES);
+  if (sw == 32)
+    FA_RED_LAUNCH((k_reduce<32, 1, EPI, W, false, true>), grid, blk, st, r);
+  else if (sw > 16)
+    FA_RED_LAUNCH((k_reduce<32, 1, EPI, W, false, false>), grid, blk, st, r);
+  else if (sw == 16)
+    FA_RED_LAUNCH((k_reduce<16, 2, EPI, W, false, true>), grid, blk, st, r);
+  else
+    FA_RED_LAUNCH((k_reduce<16, 2, EPI, W, false, false>), grid, blk, st, r);
+}
+
+// FA_WINDOWS 1: a plan of R > 1 rounds of the capped grid runs as R launches over equal column windows,
+// one round each.  Over several rounds of ~1000 clients the workgroups drift apart; a launch boundary
+// re-aligns them.  Measured interleaved on three boxes (tools/window_probe.py, profiles/r02_window_probe.log):
+// 1000 x 25 M 7.07-7.09 -> 7.15-7.16 TB/s, 1000 x 12.5 M +0.6 %; the bits are the same (columns are
+// independent).
+#ifndef FA_WINDOWS
+#define FA_WINDOWS 1
+#endif
 template <int EPI, bool W>
 static void launch_plan(const RedArgs& r, hipStream_t st) {
   int64_t col = 0;
@@ -409,6 +448,11 @@ static void launch_plan(const RedArgs& r, hipStream_t st) {
     if (sw1 > 32) {  // R rounds of the capped grid, tiles at most FA_CAP_SW_MAX strips wide
       const int64_t per_round = (int64_t)FA_RED_WAVES * FA_CAP_SW_MAX * cap;
       const int64_t R = (S + per_round - 1) / per_round;
+      if (FA_WINDOWS && FA_CAP_SW_MAX == 32) {
+        const int64_t Sw = (S + R - 1) / R;
+        for (int64_t s0 = 0; s0 < S; s0 += Sw) launch_window<EPI, W>(r, s0, S - s0 < Sw ? S - s0 : Sw, cap, st);
+        return;
+      }
       const int64_t sw = (S + (int64_t)FA_RED_WAVES * R * cap - 1) / ((int64_t)FA_RED_WAVES * R * cap);
       if (sw > 16)
         launch_balanced<32, 1, EPI, W>(r, sw, R, st);
@@ -458,6 +502,22 @@ static int launch_reduce(const RedArgs& r, hipStream_t st, const char* what) {
   else
     launch_plan<EPI, false>(r, st);
   return check_launch(what);
+}
+
+// Kernel launches one fa_reduce / fa_reduce_yogi call makes at (K, P): the plan run in counting mode.
+extern "C" int64_t fa_reduce_launches(int32_t K, int64_t P, int32_t weighted) {
+  if (K <= 0 || P <= 0) return 0;
+  RedArgs r{};
+  r.P4 = (P + 3) / 4;
+  r.K = K;
+  int64_t n = 0;
+  g_plan_count = &n;
+  if (weighted)
+    launch_plan<EPI_MEAN, true>(r, nullptr);
+  else
+    launch_plan<EPI_MEAN, false>(r, nullptr);
+  g_plan_count = nullptr;
+  return n;
 }
 
 static int check_reduce_args(const char* what, const float* x, int64_t ld, int32_t K, int64_t P,
@@ -1143,6 +1203,9 @@ extern "C" int64_t fa_qfed_workspace_bytes(int32_t K) {  // enough for either ke
 #ifndef QF_PLAIN_GLDS
 #define QF_PLAIN_GLDS 0
 #endif
+#ifndef QF_WIN_COLS
+#define QF_WIN_COLS 0  // > 0: launch rows longer than this many columns as windows of at most it (tuning knob)
+#endif
 #ifndef QF_WIDE_BYTES
 #define QF_WIDE_BYTES (1LL << 31)  // largest QF_G-row span served by one descriptor (tuning knob; <= 2^31)
 #endif
@@ -1158,7 +1221,11 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
   // WIDE needs QF_G rows plus the sentinel below 2^32; otherwise per-row descriptors over column
   // windows of 2^28 floats (1 GiB), one launch each; the gathers add their partial norms in order.
   const bool wide = (int64_t)ld * 4 * QF_G <= QF_WIDE_BYTES;
-  const int64_t win = wide ? (P > 0 ? P : 1) : (1LL << 28);
+  int64_t win = wide ? (P > 0 ? P : 1) : (1LL << 28);
+  if (QF_WIN_COLS > 0 && win > QF_WIN_COLS) {  // long rows: equal column windows of <= QF_WIN_COLS, in order
+    const int64_t n = (P + QF_WIN_COLS - 1) / QF_WIN_COLS;
+    win = ((P + n - 1) / n + 63) / 64 * 64;
+  }
   for (int64_t w0 = 0; w0 < P || w0 == 0; w0 += win) {
     QfArgs qw = q;
     const int64_t pw = P - w0 < win ? P - w0 : win;

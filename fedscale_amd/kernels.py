@@ -93,6 +93,11 @@ def qfed_max_chunk() -> int:
     return N.load().fa_qfed_max_chunk()
 
 
+def reduce_launches(K: int, P: int, weighted: bool = False) -> int:
+    """Kernel launches one fa_reduce call makes at (K, P) on the current device (fa_reduce_launches)."""
+    return int(N.load().fa_reduce_launches(int(K), int(P), 1 if weighted else 0))
+
+
 def qfed_workspace(K: int, device) -> torch.Tensor:
     nbytes = N.load().fa_qfed_workspace_bytes(K)
     return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)

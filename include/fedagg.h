@@ -62,6 +62,13 @@ int fa_reduce(const float* x, int64_t ld, int32_t K, int64_t P, const float* a, 
               float* out, float denom, int32_t flags, fa_stream_t stream);
 
 /*
+ * Number of kernel launches one fa_reduce (or fa_reduce_yogi) call makes at (K, P) on the current device:
+ * long buckets run as several launches over column windows.  For reporting per-launch figures (bench.py);
+ * no reference counterpart.  Needs a GPU (the plan depends on the CU count).
+ */
+int64_t fa_reduce_launches(int32_t K, int64_t P, int32_t weighted);
+
+/*
  * fa_reduce with FA_FINALIZE, fused with the FedYoGi server step in the same pass over HBM:
  *   cur = chain/denom; g = cur - last; m = beta*m + omb*g; v = v - (omb2*g*g)*sign(v - g*g);
  *   out = last + (reciprocal(sqrt(v) + tau) * eta) * m

@@ -79,6 +79,29 @@ def test_headline_fedavg_and_fedbuff_k1000_p25m(gpu_device):
     del x
 
 
+@pytest.mark.parametrize("weighted", [False, True])
+def test_reduce_column_windows_every_column(gpu_device, weighted):
+    """A bucket long enough for several rounds of the capped grid runs as column windows (fedagg.hip
+    FA_WINDOWS); every column, the windows' seams included, equals the host's in-order fp32 chain."""
+    from fedscale_amd import kernels as kx
+    from fedscale_amd.bucket import round_up
+
+    K, P = 8, 13_000_003
+    assert kx.reduce_launches(K, P, weighted=weighted) > 1
+    ld = round_up(P, 64)
+    rng = np.random.default_rng(7)
+    xh = rng.standard_normal((K, ld), dtype=np.float32)
+    a = rng.uniform(0.2, 1.0, K).astype(np.float32) if weighted else None
+    denom = np.float32(a.astype(np.float64).sum()) if weighted else np.float32(K)
+    x = torch.from_numpy(xh).cuda()
+    out = torch.empty(ld, device="cuda")
+    kx.reduce(x, K, P, out, a=torch.from_numpy(a).cuda() if weighted else None, denom=float(denom), finalize=True)
+    acc = xh[0, :P] * a[0] if weighted else xh[0, :P].copy()
+    for k in range(1, K):
+        acc = acc + (a[k] * xh[k, :P] if weighted else xh[k, :P])
+    np.testing.assert_array_equal(out[:P].cpu().numpy(), np.divide(acc, denom))
+
+
 def test_c4_fedyogi_k1000_p25m(gpu_device):
     """Config 4 (per-GPU shard): fused reduce + FedYoGi over 1000 x 25M, two rounds of state."""
     from fedscale_amd import kernels as kx
