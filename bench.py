@@ -567,11 +567,12 @@ def main():
         reassembly_ms = _max_over_ranks([(time.perf_counter() - t0r) * 1e3 / 5], dev, world, args.dist_backend)[0]
     alg_bytes = w.alg_bytes
     P_local, n_passes = w.P, len(w.passes)
+    w_ld = w.ld
     # launches of the dominant kernel per step: fa_reduce runs long buckets as column windows (fedagg.hip
     # FA_WINDOWS), so the per-launch figures rocprof reports are the step's divided by this
     from fedscale_amd import kernels as kx
     if policy == "qfedavg":
-        launches = n_passes
+        launches = n_passes * kx.qfed_launches(w_ld, P_local)
     else:
         launches = n_passes * kx.reduce_launches(w.C if n_passes > 1 else K, P_local, weighted=policy == "fedbuff")
     w.free()

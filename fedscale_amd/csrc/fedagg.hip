@@ -1204,12 +1204,30 @@ extern "C" int64_t fa_qfed_workspace_bytes(int32_t K) {  // enough for either ke
 #define QF_PLAIN_GLDS 0
 #endif
 #ifndef QF_WIN_COLS
-#define QF_WIN_COLS 0  // > 0: launch rows longer than this many columns as windows of at most it (tuning knob)
+#define QF_WIN_COLS ((int64_t)QF_GRID * 4 * QF_V * 256)  // one round of full-width tiles (4,194,304 columns); 0: off
 #endif
 #ifndef QF_WIDE_BYTES
 #define QF_WIDE_BYTES (1LL << 31)  // largest QF_G-row span served by one descriptor (tuning knob; <= 2^31)
 #endif
 static_assert(QF_WIDE_BYTES <= (1LL << 31), "QF_WIDE_BYTES: the rows plus the OOB sentinel must stay below 2^32");
+
+// Column window of one k_qfed_accum launch: per-row descriptors need windows of <= 2^28 columns, and long
+// rows run as windows of one round of full-width tiles (QF_WIN_COLS) — over several rounds of ~1000
+// clients the workgroups drift apart and a launch boundary re-aligns them (tools/tune_qfed2.py,
+// profiles/r02_tune_qfed_windows.log: 1000 x 25 M 6.87 -> 7.03 TB/s, 462 x 100 M 6.34 -> 6.89).  The
+// windows' gathers add their per-client partial norms in window order (deterministic; fp64).
+static int64_t qfed_window(int64_t ld, int64_t P) {
+  const bool wide = (int64_t)ld * 4 * QF_G <= QF_WIDE_BYTES;
+  int64_t win = wide ? (P > 0 ? P : 1) : (1LL << 28);
+  if (QF_WIN_COLS > 0 && win > QF_WIN_COLS) win = QF_WIN_COLS;
+  return win;
+}
+
+extern "C" int64_t fa_qfed_launches(int64_t ld, int64_t P) {
+  if (P <= 0 || ld < P) return 0;
+  const int64_t win = qfed_window(ld, P);
+  return (P + win - 1) / win;
+}
 
 static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const float* last, const float* alpha,
                         float lr, int fast, float* delta, float* chain, double* sqnorm, void* workspace,
@@ -1221,11 +1239,7 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
   // WIDE needs QF_G rows plus the sentinel below 2^32; otherwise per-row descriptors over column
   // windows of 2^28 floats (1 GiB), one launch each; the gathers add their partial norms in order.
   const bool wide = (int64_t)ld * 4 * QF_G <= QF_WIDE_BYTES;
-  int64_t win = wide ? (P > 0 ? P : 1) : (1LL << 28);
-  if (QF_WIN_COLS > 0 && win > QF_WIN_COLS) {  // long rows: equal column windows of <= QF_WIN_COLS, in order
-    const int64_t n = (P + QF_WIN_COLS - 1) / QF_WIN_COLS;
-    win = ((P + n - 1) / n + 63) / 64 * 64;
-  }
+  const int64_t win = qfed_window(ld, P);
   for (int64_t w0 = 0; w0 < P || w0 == 0; w0 += win) {
     QfArgs qw = q;
     const int64_t pw = P - w0 < win ? P - w0 : win;

@@ -93,6 +93,11 @@ def qfed_max_chunk() -> int:
     return N.load().fa_qfed_max_chunk()
 
 
+def qfed_launches(ld: int, P: int) -> int:
+    """k_qfed_accum launches one fa_qfed_accumulate call makes for rows of ld floats (fa_qfed_launches)."""
+    return int(N.load().fa_qfed_launches(int(ld), int(P)))
+
+
 def reduce_launches(K: int, P: int, weighted: bool = False) -> int:
     """Kernel launches one fa_reduce call makes at (K, P) on the current device (fa_reduce_launches)."""
     return int(N.load().fa_reduce_launches(int(K), int(P), 1 if weighted else 0))

@@ -89,6 +89,13 @@ int fa_yogi_step(const float* cur, const float* last, float* m, float* v, float*
                  float tau, float beta, float omb, float omb2, int32_t flags, fa_stream_t stream);
 
 /*
+ * Number of k_qfed_accum launches one fa_qfed_accumulate call makes for rows of ld floats and P columns:
+ * long rows run as column windows of one round of tiles (4,194,304 columns).  For reporting per-launch
+ * figures (bench.py); no reference counterpart.
+ */
+int64_t fa_qfed_launches(int64_t ld, int64_t P);
+
+/*
  * q-FedAvg phase 1 over one chunk of K (<= fa_qfed_max_chunk()) retained client updates:
  *   g_k = (last - x[k]) / lr                      (fp32 true division)
  *   delta = FA_ACCUMULATE ? delta + alpha_k*g_0 : alpha_0*g_0; delta = delta + alpha_k*g_k ...
