@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, "libfedagg.so"))
-ABI_VERSION = 1
+ABI_VERSION = 2  # fedagg.hip FA_ABI_VERSION
 
 FA_ACCUMULATE = 1
 FA_FINALIZE = 2

@@ -23,6 +23,19 @@ import torch
 ALIGN = 64  # floats: 256-byte rows, and the shard granule
 
 
+class _NullCtx:
+    __slots__ = ()
+
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NULL_CTX = _NullCtx()
+
+
 def default_pack_workers() -> int:
     """Host threads for the ingress gather (FEDAGG_PACK_WORKERS overrides; the GPU box gives a GPU 16)."""
     env = os.environ.get("FEDAGG_PACK_WORKERS")
@@ -236,7 +249,27 @@ class ClientStaging:
     BULK_MAX_BYTES = 64 << 20
 
     def __init__(self, layout: BucketLayout, device, capacity: int, ring: int = 2,
-                 pack_workers: Optional[int] = None, async_ingress: bool = False, bulk: Optional[bool] = None):
+                 pack_workers: Optional[int] = None, async_ingress: bool = False, bulk: Optional[bool] = None,
+                 dstream=None):
+        """``dstream``: the owning adapter's DeviceStream; the staging's buffers, H2D copies and events are
+        issued on it (None: the caller's current stream)."""
+        self.dstream = dstream
+        if dstream is None:
+            self._init(layout, device, capacity, ring, pack_workers, async_ingress, bulk)
+        else:
+            with dstream:
+                self._init(layout, device, capacity, ring, pack_workers, async_ingress, bulk)
+
+    def _on(self):
+        """Context for GPU work: the dstream, unless it is already current (or there is none)."""
+        ds = self.dstream
+        if ds is None:
+            return _NULL_CTX
+        from .state import DeviceStream
+
+        return _NULL_CTX if DeviceStream.current() is ds else ds
+
+    def _init(self, layout, device, capacity, ring, pack_workers, async_ingress, bulk):
         self.layout = layout
         self.pack_workers = pack_workers or default_pack_workers()
         self.device = torch.device(device)
@@ -295,8 +328,11 @@ class ClientStaging:
             return
         on_dev = [isinstance(v, torch.Tensor) and v.device == self.device for v in values]
         if all(on_dev):
-            self.drain()  # keep the slots' arrival order with any queued host copies
-            lay.pack_device(values, self.x[slot], self.xi[slot])
+            with self._on():
+                if self.dstream is not None:
+                    self.dstream.wait_caller()  # the caller's device tensors
+                self.drain()  # keep the slots' arrival order with any queued host copies
+                lay.pack_device(values, self.x[slot], self.xi[slot])
             return
         plan = lay.host_gather_plan(values)  # validation errors surface here, synchronously
         if self.bulk:
@@ -314,7 +350,7 @@ class ClientStaging:
             r[3] = None
         if r[2] is not None:
             r[2].synchronize()  # the previous H2D out of this pinned row has completed
-        stream = torch.cuda.current_stream(self._dev_index)
+        stream = self.dstream.stream if self.dstream is not None else torch.cuda.current_stream(self._dev_index)
         if self.async_ingress:
             if self._pool is None:
                 from concurrent.futures import ThreadPoolExecutor
@@ -322,7 +358,8 @@ class ClientStaging:
                 self._pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="fedagg-ingress")
             r[3] = self._pool.submit(self._copy_in, slot, plan, r, stream, False)
         else:
-            r[2] = self._copy_in(slot, plan, r, stream, True)
+            with self._on():
+                r[2] = self._copy_in(slot, plan, r, stream, True)
         self._next = (self._next + 1) % len(self._ring)
 
     def _put_row(self, slot: int, row: "HostRow"):
@@ -336,13 +373,14 @@ class ClientStaging:
                 self._hxi_np[slot, :lay.Q] = row.i_np[:lay.Q]
             self._bulk_hi = slot + 1
             return
-        self.x[slot, :lay.P].copy_(row.f[lay.p0:lay.p1], non_blocking=True)
-        if lay.Q:
-            self.xi[slot, :lay.Q].copy_(row.i[:lay.Q], non_blocking=True)
-        ev = self._row_evs.get(id(row))
-        if ev is None:
-            ev = self._row_evs[id(row)] = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(self._dev_index))
+        with self._on():  # this part's device and stream: the copy crosses this GPU's own link
+            self.x[slot, :lay.P].copy_(row.f[lay.p0:lay.p1], non_blocking=True)
+            if lay.Q:
+                self.xi[slot, :lay.Q].copy_(row.i[:lay.Q], non_blocking=True)
+            ev = self._row_evs.get(id(row))
+            if ev is None:
+                ev = self._row_evs[id(row)] = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(self._dev_index))
         row.pending.append(ev)
 
     def _put_bulk_views(self, slot: int, values) -> bool:
@@ -387,11 +425,12 @@ class ClientStaging:
     def _drain_bulk(self):
         lo, hi = self._bulk_lo, self._bulk_hi
         if hi > lo:
-            # whole rows: one contiguous block (the mirror's padding columns are zero, as on the device)
-            self.x[lo:hi].copy_(self._hx[lo:hi], non_blocking=True)
-            if self.layout.Q:
-                self.xi[lo:hi].copy_(self._hxi[lo:hi], non_blocking=True)
-            self._bulk_ev.record(torch.cuda.current_stream(self._dev_index))
+            with self._on():
+                # whole rows: one contiguous block (the mirror's padding columns are zero, as on the device)
+                self.x[lo:hi].copy_(self._hx[lo:hi], non_blocking=True)
+                if self.layout.Q:
+                    self.xi[lo:hi].copy_(self._hxi[lo:hi], non_blocking=True)
+                self._bulk_ev.record(torch.cuda.current_stream(self._dev_index))
             self._bulk_busy = True
             self._bulk_lo = self._bulk_hi = 0
 

@@ -85,15 +85,29 @@ class DeviceAggregatorMixin:
     def _is_last_result_in_round(self):
         return self.model_in_update == self.tasks_round
 
+    def _aggregation_device(self):
+        """The GPU of the reference's ``self.device`` (aggregator.py:47: ``args.cuda_device`` when
+        ``use_cuda``, e.g. "cuda:3"; None = the current device).  The device path has no CPU fallback."""
+        d = getattr(self, "device", None)
+        if d is None:
+            return None
+        import torch
+
+        d = torch.device(d) if not isinstance(d, int) else torch.device("cuda", d)
+        if d.type != "cuda":
+            raise ValueError(f"the aggregator device is {d} (use_cuda=False?): the device aggregation path runs on "
+                             f"a GPU only; set use_cuda and cuda_device, or use the reference Aggregator")
+        return d
+
     def init_model(self):
-        """aggregator.py:198-211, re-wired onto the device adapter + device server optimizer.  With
-        ``device_shards`` (or FEDAGG_DEVICES="0,1,...") naming more than one GPU, the model is sharded over
-        them inside this one process (``ShardedModelAdapter``)."""
+        """aggregator.py:198-211, re-wired onto the device adapter + device server optimizer, on the GPU the
+        reference's ``--cuda_device`` selects (``self.device``, aggregator.py:47).  With ``device_shards``
+        (or FEDAGG_DEVICES="0,1,...") naming more than one GPU, the model is sharded over them inside this
+        one process (``ShardedModelAdapter``)."""
         from .optimizers import TorchServerOptimizer
 
         super().init_model()
         model = self.model_wrapper.get_model()
-        opt = TorchServerOptimizer(self.args.gradient_policy, self.args, self.device)
         devs = self.device_shards
         if devs is None:
             import os
@@ -103,10 +117,12 @@ class DeviceAggregatorMixin:
         if devs is not None and len(devs) > 1:
             from ..internal.sharded_model_adapter import ShardedModelAdapter
 
+            opt = TorchServerOptimizer(self.args.gradient_policy, self.args, devs[0])
             self.model_wrapper = ShardedModelAdapter(model, optimizer=opt, devices=devs)
         else:
-            self.model_wrapper = TorchModelAdapter(model, optimizer=opt,
-                                                   device=devs[0] if devs else None)
+            dev = devs[0] if devs else self._aggregation_device()
+            opt = TorchServerOptimizer(self.args.gradient_policy, self.args, dev)
+            self.model_wrapper = TorchModelAdapter(model, optimizer=opt, device=dev)
 
     def _wrapper(self) -> TorchModelAdapter:
         w = self.model_wrapper

@@ -58,6 +58,10 @@ class TorchServerOptimizer(object):
 
     # ---- device path (FlatState in, adapter out) -------------------------------------------------
     def _device_step(self, last: FlatState, current: FlatState, adapter, results):
+        with adapter.dstream.joined():  # the adapter's GPU and stream (set_weights already entered them)
+            self._device_step_on_stream(last, current, adapter, results)
+
+    def _device_step_on_stream(self, last: FlatState, current: FlatState, adapter, results):
         lay = last.layout
         out_f, out_s = adapter._scratch_buffers()
         if self.mode == "fed-yogi":
@@ -70,15 +74,23 @@ class TorchServerOptimizer(object):
         else:
             rnd = results
             if not isinstance(rnd, DeviceRound):
-                rnd = self._stage_results(lay, last, results)
+                rnd = self._stage_results(lay, last, results, dstream=adapter.dstream)
             rnd.finalize_qfed(out=out_f, model_side=out_s, sqnorm_allreduce=adapter._sqnorm_allreduce())
         adapter._commit_scratch()
 
-    def _stage_results(self, lay: BucketLayout, last: FlatState, results) -> DeviceRound:
+    def _stage_results(self, lay: BucketLayout, last: FlatState, results, dstream=None) -> DeviceRound:
         """q-FedAvg from the reference's retained list of result dicts (aggregator.py:466-467)."""
-        rnd = DeviceRound(lay, last.f32.device, len(results), "qfedavg", last_f32=last.f32, last_i64=last.side)
+        from .aggregator import StagedUpload
+
+        rnd = DeviceRound(lay, last.f32.device, len(results), "qfedavg", last_f32=last.f32, last_i64=last.side,
+                          dstream=dstream)
         lr, q = self.args.learning_rate, self.args.qfed_q
         for res in results:
+            if isinstance(res["update_weight"], StagedUpload):
+                raise RuntimeError(
+                    "a retained q-FedAvg result's update_weight was released after it was staged in HBM "
+                    "(DeviceAggregatorMixin.device_release_uploads); only the device round can consume it — "
+                    "set device_release_uploads = False to keep the host arrays for this set_weights path")
             rnd.add(res["update_weight"], loss=res["moving_loss"], learning_rate=lr, q=q)
         return rnd
 

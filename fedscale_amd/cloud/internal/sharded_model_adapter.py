@@ -13,8 +13,10 @@ loop.  ``ShardedModelAdapter`` keeps the reference interface of ``TorchModelAdap
   YoGi m/v, the replicated int64 side table);
 * ingress: an upload is gathered ONCE into a pinned row of the whole model (``HostRow``) and each part
   copies its slice to its own device — one H2D per GPU, over the GPUs' own PCIe links;
-* the per-part reductions run on each device's stream, independently (FedAvg, FedBuff and fused FedYoGi
-  need no cross-device step: every output element depends only on its own column);
+* the per-part reductions run on each part's own stream of its own device (``DeviceStream``: the part's GPU is
+  made current for every call, so a part's kernels can never land on another GPU or on the null stream),
+  independently (FedAvg, FedBuff and fused FedYoGi need no cross-device step: every output element depends
+  only on its own column);
 * q-FedAvg's one exchange, the per-client squared norms summed over the shards (optimizers.py:96-97), is
   an RCCL all-gather over xGMI issued for all devices at once, followed by a fixed-order sum on every
   device (``DeviceGroup.sum_f64``), so the result does not depend on the transport;
@@ -73,6 +75,7 @@ class ShardedModelAdapter(TorchModelAdapter):
         self.model = model
         self.optimizer = optimizer
         self.device = self.group.devices[0]
+        self.dstream = self.group.streams[0]
         self.shards = ShardGroup()  # this process is one rank; its parts are in self.parts
         self.layout = BucketLayout.from_state_dict(model.state_dict())  # the whole model (host side)
         self.staging_capacity = staging_capacity
@@ -80,7 +83,7 @@ class ShardedModelAdapter(TorchModelAdapter):
         for r, dev in enumerate(self.group.devices):
             opt = optimizer.for_shard(dev) if optimizer is not None else None
             self.parts.append(TorchModelAdapter(model, optimizer=opt, device=dev, shards=PartOf(r, N, self.group),
-                                                staging_capacity=staging_capacity))
+                                                staging_capacity=staging_capacity, dstream=self.group.streams[r]))
         self._rows = []
         self._next_row = 0
         self.pack_workers = default_pack_workers()
@@ -158,12 +161,19 @@ class ShardedModelAdapter(TorchModelAdapter):
         if opt is not None and is_aggregator and getattr(opt, "mode", None) == "q-fedavg":
             rnd = self.begin_round(len(client_training_results), "qfedavg")
             a = opt.args
+            from ..aggregation.aggregator import StagedUpload
+
             for res in client_training_results:
+                if isinstance(res["update_weight"], StagedUpload):
+                    raise RuntimeError("a retained q-FedAvg result's update_weight was released after it was "
+                                       "staged in HBM (device_release_uploads); set_weights cannot re-stage it")
                 rnd.add(res["update_weight"], loss=res["moving_loss"], learning_rate=a.learning_rate, q=a.qfed_q)
             self._apply_qfed(rnd)
             for p in self.parts:  # the reference's model_weights: the list it was handed
-                p._mean_f = torch.zeros(p.layout.ld, dtype=torch.float32, device=p.device)
-                p._pack_values(weights, p._mean_f, p._mean_s)
+                with p.dstream.joined():
+                    p.dstream.wait_caller()
+                    p._mean_f = torch.zeros(p.layout.ld, dtype=torch.float32, device=p.device)
+                    p._pack_values(weights, p._mean_f, p._mean_s)
                 p._mean_valid, p._mean_round = True, None
         else:
             for p in self.parts:
@@ -190,11 +200,12 @@ class ShardedModelAdapter(TorchModelAdapter):
         f_cpu = np.empty(max(1, L.P_full), dtype=np.float32)
         s_cpu = None
         for p in self.parts:
-            mean_f, mean_s = p._mean_device()
-            if p.layout.P:
-                f_cpu[p.layout.p0:p.layout.p1] = mean_f[:p.layout.P].cpu().numpy()
-            if s_cpu is None:
-                s_cpu = mean_s[:L.Q].cpu().numpy()
+            with p.dstream.joined():  # the D2H copies run on the stream that computed the part's mean
+                mean_f, mean_s = p._mean_device()
+                if p.layout.P:
+                    f_cpu[p.layout.p0:p.layout.p1] = mean_f[:p.layout.P].cpu().numpy()
+                if s_cpu is None:
+                    s_cpu = mean_s[:L.Q].cpu().numpy()
         return self._mean_lists(f_cpu, s_cpu)
 
     # the server optimizer's YoGi state lives in the parts (one m/v slice per device)

@@ -27,7 +27,7 @@ import torch
 from ...bucket import BucketLayout, ClientStaging
 from ...kernels import qfed_max_chunk as kx_qfed_max_chunk
 from ...round import DeviceRound, default_capacity
-from ...state import FlatState, ShardGroup
+from ...state import DeviceStream, FlatState, ShardGroup
 from .model_adapter_base import ModelAdapterBase
 
 
@@ -117,11 +117,19 @@ def _resolve_device(device) -> torch.device:
 
 
 class TorchModelAdapter(ModelAdapterBase):
+    """``dstream``: the ``DeviceStream`` (GPU + HIP stream) every kernel, copy and event of this adapter is
+    issued on — made for ``device`` when not given; a ``ShardedModelAdapter`` hands each part its own.  Each
+    public call runs under ``dstream.joined()``: the adapter's GPU is current for the call (whatever the
+    caller had current) and the caller's stream on that GPU is ordered after the call's work."""
+
     def __init__(self, model: torch.nn.Module, optimizer=None, device=None, shards: Optional[ShardGroup] = None,
-                 staging_capacity: Optional[int] = None, _load_from=None):
+                 staging_capacity: Optional[int] = None, _load_from=None, dstream: Optional[DeviceStream] = None):
         self.model = model
         self.optimizer = optimizer
         self.device = _resolve_device(device)
+        if dstream is not None and dstream.device != self.device:
+            raise ValueError(f"dstream is on {dstream.device}, the adapter on {self.device}")
+        self.dstream = dstream if dstream is not None else DeviceStream(self.device)
         self.shards = shards or ShardGroup()
         sd = model.state_dict()
         if self.shards.shards_params:
@@ -129,22 +137,25 @@ class TorchModelAdapter(ModelAdapterBase):
         else:  # single GPU, or client mode: every rank holds the whole model
             self.layout = BucketLayout.from_state_dict(sd)
         L, dev = self.layout, self.device
-        self._f = [torch.zeros(L.ld, dtype=torch.float32, device=dev) for _ in range(2)]
-        self._s = [torch.zeros(L.ldq, dtype=torch.int64, device=dev) for _ in range(2)]
-        self._cur = 0
-        # float64 side table + fp32 mean of the last round: the reference's Aggregator.model_weights
-        self._mean_s = torch.zeros(L.ldq, dtype=torch.float64, device=dev)
-        self._mean_f: Optional[torch.Tensor] = None
-        self._mean_valid = False
-        self.staging: Optional[ClientStaging] = None
-        self.staging_capacity = staging_capacity
-        cur_f = torch.zeros(L.ld, dtype=torch.float32, device=dev)
-        cur_s = torch.zeros(L.ldq, dtype=torch.float64, device=dev)
-        self._pack_values(list(_load_from) if _load_from is not None else list(sd.values()), cur_f, cur_s)
-        self._f[0].copy_(cur_f)
-        self._s[0].copy_(cur_s.to(torch.int64))
-        self._ready = torch.cuda.Event()  # the kernels that wrote the current model buffers
-        self._ready_stream = torch.cuda.current_stream(self.device)
+        with self.dstream.joined():
+            self.dstream.wait_caller()  # _load_from may hold the caller's device tensors
+            self._f = [torch.zeros(L.ld, dtype=torch.float32, device=dev) for _ in range(2)]
+            self._s = [torch.zeros(L.ldq, dtype=torch.int64, device=dev) for _ in range(2)]
+            self._cur = 0
+            # float64 side table + fp32 mean of the last round: the reference's Aggregator.model_weights
+            self._mean_s = torch.zeros(L.ldq, dtype=torch.float64, device=dev)
+            self._mean_f: Optional[torch.Tensor] = None
+            self._mean_valid = False
+            self.staging: Optional[ClientStaging] = None
+            self.staging_capacity = staging_capacity
+            cur_f = torch.zeros(L.ld, dtype=torch.float32, device=dev)
+            cur_s = torch.zeros(L.ldq, dtype=torch.float64, device=dev)
+            self._pack_values(list(_load_from) if _load_from is not None else list(sd.values()), cur_f, cur_s)
+            self._f[0].copy_(cur_f)
+            self._s[0].copy_(cur_s.to(torch.int64))
+            self._ready = torch.cuda.Event()  # the kernels that wrote the current model buffers
+            self._ready.record(self.dstream.stream)
+            self._ready_stream = self.dstream.stream
         self._init_egress(_load_from is None)
 
     def _init_egress(self, module_in_sync: bool):
@@ -168,7 +179,7 @@ class TorchModelAdapter(ModelAdapterBase):
         return self._f[1 - self._cur], self._s[1 - self._cur]
 
     def _commit_scratch(self):
-        self._ready_stream = torch.cuda.current_stream(self.device)
+        self._ready_stream = self.dstream.stream  # every write to the model buffers is issued on it
         self._ready.record(self._ready_stream)
         with self._egress_lock:  # (buffer, version) flip atomically for the servicer threads
             self._cur = 1 - self._cur
@@ -198,20 +209,22 @@ class TorchModelAdapter(ModelAdapterBase):
     # ---- reference API --------------------------------------------------------------------------
     def set_weights(self, weights, is_aggregator=True, client_training_results=None):
         """torch_model_adapter.py:23-39 on the device."""
-        L = self.layout
-        last = self._snapshot()
-        cur_f = torch.zeros(L.ld, dtype=torch.float32, device=self.device)
-        cur_s = torch.zeros(L.ldq, dtype=torch.float64, device=self.device)
-        self._pack_values(list(weights), cur_f, cur_s)
-        self._mean_f, self._mean_s, self._mean_valid = cur_f, cur_s, True
-        opt = self.optimizer
-        if opt is not None and is_aggregator and getattr(opt, "mode", None) in ("fed-yogi", "q-fedavg"):
-            opt.update_round_gradient(last, FlatState(L, cur_f, cur_s), self, client_training_results)
-            return
-        nf, ns = self._scratch_buffers()
-        nf.copy_(cur_f)
-        ns.copy_(cur_s.to(torch.float32).to(torch.int64))  # float32 -> int64 load truncates (:31-35)
-        self._commit_scratch()
+        with self.dstream.joined():
+            self.dstream.wait_caller()  # weights may be the caller's device tensors
+            L = self.layout
+            last = self._snapshot()
+            cur_f = torch.zeros(L.ld, dtype=torch.float32, device=self.device)
+            cur_s = torch.zeros(L.ldq, dtype=torch.float64, device=self.device)
+            self._pack_values(list(weights), cur_f, cur_s)
+            self._mean_f, self._mean_s, self._mean_valid = cur_f, cur_s, True
+            opt = self.optimizer
+            if opt is not None and is_aggregator and getattr(opt, "mode", None) in ("fed-yogi", "q-fedavg"):
+                opt.update_round_gradient(last, FlatState(L, cur_f, cur_s), self, client_training_results)
+                return
+            nf, ns = self._scratch_buffers()
+            nf.copy_(cur_f)
+            ns.copy_(cur_s.to(torch.float32).to(torch.int64))  # float32 -> int64 load truncates (:31-35)
+            self._commit_scratch()
 
     def _copy_to_host(self, f_cpu: torch.Tensor, s_cpu: torch.Tensor):
         """D2H of the current model into pinned f_cpu[:P_full] / s_cpu[:Q] (the caller holds the egress
@@ -344,6 +357,10 @@ class TorchModelAdapter(ModelAdapterBase):
         """``keep_mean`` for q-FedAvg rounds: True fuses the FedAvg chain when the round spans several chunks
         (the staged updates are then gone by the end of the round), "always" in every round (the mean is then
         independent of the staging's later reuse), False never (model_weights of such rounds raises)."""
+        with self.dstream.joined():
+            return self._begin_round(K, policy, capacity, keep_mean)
+
+    def _begin_round(self, K, policy, capacity, keep_mean) -> DeviceRound:
         cap = capacity or self.staging_capacity
         K_local = K
         if self.shards.shards_clients:  # this rank stages only its block of the arrivals
@@ -359,16 +376,21 @@ class TorchModelAdapter(ModelAdapterBase):
             want = min(want, kx_qfed_max_chunk())
         if self.staging is None or self.staging.capacity < want:
             self.staging = None
-            self.staging = ClientStaging(self.layout, self.device, want)
+            self.staging = ClientStaging(self.layout, self.device, want, dstream=self.dstream)
         snap = self._snapshot()
         chain = keep_mean == "always" or (bool(keep_mean) and want < K_local)
         return DeviceRound(self.layout, self.device, K, policy, capacity=want, staging=self.staging,
                            last_f32=snap.f32, last_i64=snap.side,
-                           clients=self.shards if self.shards.shards_clients else None, mean_chain=chain)
+                           clients=self.shards if self.shards.shards_clients else None, mean_chain=chain,
+                           dstream=self.dstream)
 
     def apply_round(self, rnd: DeviceRound, denom32: float, denom64: float, client_training_results=None,
                     keep_mean: bool = True):
         """Finish a round: reduce the last chunk with the server step fused, then swap buffers."""
+        with self.dstream.joined():
+            self._apply_round(rnd, denom32, denom64, keep_mean)
+
+    def _apply_round(self, rnd: DeviceRound, denom32: float, denom64: float, keep_mean):
         L = self.layout
         last = self._snapshot()
         out_f, out_s = self._scratch_buffers()
@@ -407,11 +429,12 @@ class TorchModelAdapter(ModelAdapterBase):
 
     def _finish_qfed(self, rnd: DeviceRound):
         """hs + step of a folded q-FedAvg round (its norms already summed over the shards), then commit."""
-        out_f, out_s = self._scratch_buffers()
-        rnd.qfed_finish(out=out_f, model_side=out_s)
-        self._mean_valid = False
-        self._mean_round = rnd  # the mean can still be recomputed lazily from the staged updates
-        self._commit_scratch()
+        with self.dstream.joined():
+            out_f, out_s = self._scratch_buffers()
+            rnd.qfed_finish(out=out_f, model_side=out_s)
+            self._mean_valid = False
+            self._mean_round = rnd  # the mean can still be recomputed lazily from the staged updates
+            self._commit_scratch()
 
     def round_mean_weights(self):
         """The reference's Aggregator.model_weights after the last result of a round (the FedAvg mean,
@@ -419,10 +442,11 @@ class TorchModelAdapter(ModelAdapterBase):
         return LazyWeights(self)
 
     def _fetch_mean(self) -> list:
-        mean_f, mean_s = self._mean_device()
-        L = self.layout
-        full = self.shards.all_gather(mean_f[:L.ld])
-        return self._mean_lists(full[:L.P_full].to("cpu").numpy(), mean_s[:L.Q].to("cpu").numpy())
+        with self.dstream.joined():  # the D2H copies run on the stream that computed the mean
+            mean_f, mean_s = self._mean_device()
+            L = self.layout
+            full = self.shards.all_gather(mean_f[:L.ld])
+            return self._mean_lists(full[:L.P_full].to("cpu").numpy(), mean_s[:L.Q].to("cpu").numpy())
 
     def _mean_lists(self, f_cpu, s_cpu) -> list:
         out = []
@@ -432,7 +456,11 @@ class TorchModelAdapter(ModelAdapterBase):
         return out
 
     def _mean_device(self):
-        """(fp32 mean slice, float64 side mean) of the last round on this device."""
+        """(fp32 mean slice, float64 side mean) of the last round on this device (written on ``dstream``)."""
+        with self.dstream.joined():
+            return self._mean_device_on_stream()
+
+    def _mean_device_on_stream(self):
         rnd = getattr(self, "_mean_round", None)
         if not self._mean_valid and rnd is not None:
             L = self.layout

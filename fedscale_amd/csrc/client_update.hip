@@ -25,6 +25,7 @@
 #include <stdio.h>
 
 #include "../../include/fedclient.h"
+#include "fa_device.h"
 
 // error plumbing shared with fedagg.hip (thread-local last-error string)
 extern "C" __attribute__((visibility("hidden"))) int fa_internal_set_error(int code, const char* msg);
@@ -442,6 +443,13 @@ int check_list(const char* what, int32_t T, float* const* a, const float* const*
   return FA_OK;
 }
 
+// the device a pointer-table call works on: its first non-empty tensor's (fa_device.h)
+const void* first_ptr(int32_t T, const void* const* a, const int64_t* n) {
+  for (int i = 0; a && n && i < T; ++i)
+    if (n[i] > 0 && a[i]) return a[i];
+  return nullptr;
+}
+
 int64_t total_blocks(int32_t T, const int64_t* n) {
   int64_t s = 0;
   for (int i = 0; i < T; ++i) s += (n[i] + MT_CHUNK - 1) / MT_CHUNK;
@@ -457,6 +465,7 @@ extern "C" int fa_prox_update(float* const* param, const float* const* global, c
                               float c, fa_stream_t stream) {
   int rc = check_list("fa_prox_update", T, param, global, numel, true);
   if (rc) return rc;
+  FA_DEVICE_SCOPE("fa_prox_update", stream, first_ptr(T, (const void* const*)param, numel));
   int32_t t = 0;
   while (t < T) {
     MtList L;
@@ -486,6 +495,7 @@ static int sgd_groups(const char* what, float* const* param, const float* const*
     if ((flags[i] & SGD_NESTEROV) && (momentum[i] <= 0.f || dampening[i] != 0.0))
       return fail(FA_E_ARG, "%s: tensor %d: nesterov needs momentum > 0 and zero dampening", what, i);
   }
+  FA_DEVICE_SCOPE(what, stream, first_ptr(T, (const void* const*)param, numel));
   int32_t t = 0;
   while (t < T) {
     SgdList L;
@@ -568,6 +578,7 @@ extern "C" int fa_dp_clip_coef(const float* const* param, const float* const* la
   if ((uintptr_t)workspace & 7u) return fail(FA_E_ARG, "fa_dp_clip_coef: workspace must be 8-byte aligned");
   const int64_t nblk = total_blocks(T, numel);
   if (nblk > INT32_MAX / 2) return fail(FA_E_RANGE, "fa_dp_clip_coef: model too large");
+  FA_DEVICE_SCOPE("fa_dp_clip_coef", stream, coef_out);
   double* part = (double*)workspace;
   double* tsum = part + nblk;
   hipStream_t s = (hipStream_t)stream;
@@ -602,6 +613,7 @@ extern "C" int fa_dp_apply(float* const* param, const float* const* last, float*
   for (int i = 0; !scale_only && i < T; ++i)
     if (numel[i] > 0 && (!upload[i] || ((uintptr_t)upload[i] & 3u)))
       return fail(FA_E_ARG, "fa_dp_apply: tensor %d: bad upload pointer", i);
+  FA_DEVICE_SCOPE("fa_dp_apply", stream, coef);
   int32_t t = 0;
   hipStream_t s = (hipStream_t)stream;
   const int wp = (flags & FA_DP_WRITE_PARAM) ? 1 : 0;
@@ -628,6 +640,7 @@ extern "C" int fa_dp_noise_i64(const int64_t* const* x, double* const* out, cons
       return fail(FA_E_ARG, "fa_dp_noise_i64: tensor %d: pointers must be 8-byte aligned", i);
     if (numel[i] > MT_CHUNK * (int64_t)(INT32_MAX / 4)) return fail(FA_E_RANGE, "fa_dp_noise_i64: tensor %d too large", i);
   }
+  FA_DEVICE_SCOPE("fa_dp_noise_i64", stream, first_ptr(T, (const void* const*)out, numel));
   int32_t t = 0;
   int rc;
   while (t < T) {
@@ -650,6 +663,7 @@ __global__ void k_dp_normals(float* out, int64_t n, uint64_t seed, int64_t off) 
 extern "C" int fa_dp_normals(float* out, int64_t n, uint64_t seed, int64_t noise_offset, fa_stream_t stream) {
   if (n < 0 || (n > 0 && !out)) return fail(FA_E_ARG, "fa_dp_normals: bad args");
   if (n == 0) return FA_OK;
+  FA_DEVICE_SCOPE("fa_dp_normals", stream, out);
   int64_t g = (n + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(k_dp_normals, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, out, n, seed, noise_offset);

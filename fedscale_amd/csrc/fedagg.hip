@@ -30,8 +30,11 @@
 #include <vector>
 
 #include "../../include/fedagg.h"
+#include "fa_device.h"
 
-#define FA_ABI_VERSION 1
+// 2: fa_qfed_accumulate gained `chain`, fa_sgd_prox_step's dampening became double, and every launching
+//    entry point resolves its device from the stream / output pointer (fa_device.h)
+#define FA_ABI_VERSION 2
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -281,10 +284,12 @@ __global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
 #define FA_GRID_CAP_PCT 75  // concurrent V=32 workgroups as a percentage of the CU count
 #endif
 
+// CU count and occupancy of the device the running entry point works on (its DevScope), not the thread's
+// current device
 static int cu_count() {
   static int cache[64];  // per device ordinal (idempotent, benign race)
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  const int dev = fa_scope_device();
+  if (dev < 0 || dev >= 64) return 0;
   if (cache[dev] > 0) return cache[dev];
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
@@ -295,8 +300,8 @@ static int cu_count() {
 template <int V, int U, int EPI, bool W>
 static int resident_blocks() {
   static int cache[64];  // per device ordinal: occupancy x CU count (idempotent, benign race)
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  const int dev = fa_scope_device();
+  if (dev < 0 || dev >= 64) return 0;
   if (cache[dev] > 0) return cache[dev];
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
@@ -541,6 +546,7 @@ extern "C" int fa_reduce(const float* x, int64_t ld, int32_t K, int64_t P, const
   RedArgs r{};
   r.x = x; r.ld4 = ld / 4; r.P4 = (P + 3) / 4; r.K = K; r.flags = flags; r.a = a; r.acc_in = acc_in;
   r.out = out; r.denom = denom;
+  FA_DEVICE_SCOPE("fa_reduce", stream, out);
   hipStream_t st = (hipStream_t)stream;
   if (flags & FA_FINALIZE) return launch_reduce<EPI_MEAN>(r, st, "fa_reduce");
   return launch_reduce<EPI_CHAIN>(r, st, "fa_reduce");
@@ -556,6 +562,7 @@ extern "C" int fa_reduce_yogi(const float* x, int64_t ld, int32_t K, int64_t P, 
   if (!aligned16(last) || !aligned16(m) || !aligned16(v) || !aligned16(mean_out))
     return fail(FA_E_ARG, "fa_reduce_yogi: last/m/v must be 16-byte aligned");
   if (P == 0) return FA_OK;
+  FA_DEVICE_SCOPE("fa_reduce_yogi", stream, out);
   RedArgs r{};
   r.x = x; r.ld4 = ld / 4; r.P4 = (P + 3) / 4; r.K = K; r.flags = flags; r.a = a; r.acc_in = acc_in;
   r.out = out; r.denom = denom; r.last = last; r.m = m; r.v = v; r.mean_out = mean_out;
@@ -594,6 +601,7 @@ extern "C" int fa_yogi_step(const float* cur, const float* last, float* m, float
   if (!cur || !last || !m || !v || !out) return fail(FA_E_ARG, "fa_yogi_step: NULL pointer");
   if (!aligned16(cur) || !aligned16(last) || !aligned16(m) || !aligned16(v) || !aligned16(out))
     return fail(FA_E_ARG, "fa_yogi_step: pointers must be 16-byte aligned");
+  FA_DEVICE_SCOPE("fa_yogi_step", stream, out);
   const int64_t P4 = (P + 3) / 4;
   hipLaunchKernelGGL(k_yogi_step, dim3(stride_grid(P4)), dim3(256), 0, (hipStream_t)stream,
                      (const f4*)cur, (const f4*)last, (f4*)m, (f4*)v, (f4*)out, P4, eta, tau, beta, omb, omb2,
@@ -1323,6 +1331,7 @@ extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t
   if (!aligned16(x) || !aligned16(last) || !aligned16(delta) || !aligned16(chain))
     return fail(FA_E_ARG, "fa_qfed_accumulate: x/last/delta/chain must be 16-byte aligned");
   if (!(lr > 1e-30f && lr < 1e30f)) return fail(FA_E_ARG, "fa_qfed_accumulate: lr=%g outside (1e-30, 1e30)", (double)lr);
+  FA_DEVICE_SCOPE("fa_qfed_accumulate", stream, delta);
   hipStream_t st = (hipStream_t)stream;
   const int fast = (lr >= 9.5367432e-07f && lr <= 1048576.f) ? 1 : 0;  // [2^-20, 2^20]
   const int kern = chain ? QF_CHAIN_KERNEL : QF_KERNEL;
@@ -1368,6 +1377,7 @@ __global__ __launch_bounds__(256) void k_qfed_hs(const double* sqnorm, const flo
 extern "C" int fa_qfed_hs(const double* sqnorm, const float* c1, const float* c2, int32_t K, float* hs_out,
                           fa_stream_t stream) {
   if (K < 0 || !sqnorm || !c1 || !c2 || !hs_out) return fail(FA_E_ARG, "fa_qfed_hs: bad arguments");
+  FA_DEVICE_SCOPE("fa_qfed_hs", stream, hs_out);
   hipLaunchKernelGGL(k_qfed_hs, dim3(1), dim3(256), 0, (hipStream_t)stream, sqnorm, c1, c2, (int)K, hs_out);
   return check_launch("fa_qfed_hs");
 }
@@ -1392,6 +1402,7 @@ extern "C" int fa_qfed_finalize(const float* last, const float* delta, const flo
   if (!aligned16(last) || !aligned16(delta) || !aligned16(out))
     return fail(FA_E_ARG, "fa_qfed_finalize: pointers must be 16-byte aligned");
   if (P == 0) return FA_OK;
+  FA_DEVICE_SCOPE("fa_qfed_finalize", stream, out);
   const int64_t P4 = (P + 3) / 4;
   hipLaunchKernelGGL(k_qfed_finalize, dim3(stride_grid(P4)), dim3(256), 0, (hipStream_t)stream,
                      (const f4*)last, (const f4*)delta, hs_dev, (f4*)out, P4);
@@ -1399,7 +1410,7 @@ extern "C" int fa_qfed_finalize(const float* last, const float* delta, const flo
 }
 
 // fixed-order sum of per-shard fp64 rows (after an all-gather of the shards' partial norms)
-__global__ __launch_bounds__(256) void k_sum_rows_f64(const double* __restrict__ x, int64_t ld, int n, int64_t K,
+__global__ __launch_bounds__(256) void k_sum_rows_f64(const double* x, int64_t ld, int n, int64_t K,
                                                      double* out) {
   for (int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x; k < K; k += (int64_t)gridDim.x * 256) {
     double s = x[k];
@@ -1411,6 +1422,7 @@ __global__ __launch_bounds__(256) void k_sum_rows_f64(const double* __restrict__
 extern "C" int fa_sum_rows_f64(const double* x, int64_t ld, int32_t n, int64_t K, double* out, fa_stream_t stream) {
   if (n < 1 || K < 0 || ld < K || !x || !out) return fail(FA_E_ARG, "fa_sum_rows_f64: bad arguments");
   if (K == 0) return FA_OK;
+  FA_DEVICE_SCOPE("fa_sum_rows_f64", stream, out);
   hipLaunchKernelGGL(k_sum_rows_f64, dim3(stride_grid(K)), dim3(256), 0, (hipStream_t)stream, x, ld, (int)n, K, out);
   return check_launch("fa_sum_rows_f64");
 }
@@ -1443,6 +1455,7 @@ extern "C" int fa_side_accumulate(const int64_t* xi, int32_t ldq, int32_t K, int
   if (mode == 1 && (!acc_d || !w)) return fail(FA_E_ARG, "fa_side_accumulate: acc_d/w NULL");
   if (mode != 0 && mode != 1) return fail(FA_E_ARG, "fa_side_accumulate: mode %d", (int)mode);
   if (K == 0) return FA_OK;
+  FA_DEVICE_SCOPE("fa_side_accumulate", stream, mode == 0 ? (const void*)acc_i : (const void*)acc_d);
   hipLaunchKernelGGL(k_side_accum, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, xi, ldq, K, Q, mode, w,
                      acc_i, acc_d, (flags & FA_ACCUMULATE) ? 1 : 0);
   return check_launch("fa_side_accumulate");
@@ -1461,6 +1474,7 @@ extern "C" int fa_side_close(const int64_t* acc_i, const double* acc_d, int32_t 
                              double* cur, int64_t* model, fa_stream_t stream) {
   if (Q == 0) return FA_OK;
   if (Q < 0 || (mode == 0 && !acc_i) || (mode == 1 && !acc_d)) return fail(FA_E_ARG, "fa_side_close: bad args");
+  FA_DEVICE_SCOPE("fa_side_close", stream, mode == 0 ? (const void*)acc_i : (const void*)acc_d);
   hipLaunchKernelGGL(k_side_close, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, acc_i, acc_d, Q, mode,
                      denom, cur, model);
   return check_launch("fa_side_close");
@@ -1491,6 +1505,7 @@ extern "C" int fa_side_yogi(const double* cur, const int64_t* last, double* m, d
                             int32_t flags, fa_stream_t stream) {
   if (Q == 0) return FA_OK;
   if (Q < 0 || !cur || !m || !v) return fail(FA_E_ARG, "fa_side_yogi: bad args");
+  FA_DEVICE_SCOPE("fa_side_yogi", stream, m);
   hipLaunchKernelGGL(k_side_yogi, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, cur, last, m, v, step,
                      model, Q, eta, tau, beta, omb, omb2, (flags & FA_YOGI_INIT) ? 1 : 0);
   return check_launch("fa_side_yogi");
@@ -1533,6 +1548,7 @@ extern "C" int fa_side_qfed_accumulate(const int64_t* xi, int32_t ldq, int32_t K
   if (Q == 0 || K == 0) return FA_OK;
   if (Q < 0 || K < 0 || ldq < Q || !xi || !last || !alpha || !delta_s || !sqnorm)
     return fail(FA_E_ARG, "fa_side_qfed_accumulate: bad args");
+  FA_DEVICE_SCOPE("fa_side_qfed_accumulate", stream, delta_s);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_side_qfed_delta, dim3((Q + 63) / 64), dim3(64), 0, st, xi, ldq, K, Q, last, alpha, lr, delta_s,
                      (flags & FA_ACCUMULATE) ? 1 : 0);
@@ -1553,6 +1569,7 @@ extern "C" int fa_side_qfed_finalize(const int64_t* last, const float* delta_s, 
                                      int32_t Q, fa_stream_t stream) {
   if (Q == 0) return FA_OK;
   if (Q < 0 || !last || !delta_s || !hs_dev || !model) return fail(FA_E_ARG, "fa_side_qfed_finalize: bad args");
+  FA_DEVICE_SCOPE("fa_side_qfed_finalize", stream, model);
   hipLaunchKernelGGL(k_side_qfed_finalize, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, last, delta_s,
                      hs_dev, model, Q);
   return check_launch("fa_side_qfed_finalize");
@@ -1591,6 +1608,7 @@ extern "C" int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uin
   if (K < 0 || P < 0 || ld < P || !x) return fail(FA_E_ARG, "fa_fill_synthetic: bad args");
   if (K == 0 || ld == 0) return FA_OK;
   if (K > 65535) return fail(FA_E_RANGE, "fa_fill_synthetic: K=%d > 65535 per call", (int)K);
+  FA_DEVICE_SCOPE("fa_fill_synthetic", stream, x);
   int64_t gx = (ld + 255) / 256;
   if (gx > 2048) gx = 2048;
   hipLaunchKernelGGL(k_fill, dim3((unsigned)gx, (unsigned)K), dim3(256), 0, (hipStream_t)stream, x, ld, K, P, seed, k0,
@@ -1820,6 +1838,7 @@ extern "C" int fa_prefix_box_combine(const float* xs, const int64_t* desc, int32
   if (!xs || !desc || !tensors || !chunk_tensor || !chunk_first || !global)
     return fail(FA_E_ARG, "fa_prefix_box_combine: NULL pointer");
   if (!aligned16(xs)) return fail(FA_E_ARG, "fa_prefix_box_combine: xs must be 16-byte aligned");
+  FA_DEVICE_SCOPE("fa_prefix_box_combine", stream, xs);
   const int grid = (HB_GRID > 0 && nchunks > HB_GRID) ? HB_GRID : nchunks;
   hipLaunchKernelGGL(k_prefix_box, dim3(grid), dim3(256), 0, (hipStream_t)stream, xs, desc, (int)K, (int)T, tensors,
                      chunk_tensor, chunk_first, global, (int)nchunks);

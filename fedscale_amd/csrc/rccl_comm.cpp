@@ -18,6 +18,7 @@
 #include <new>
 #include <vector>
 
+#include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include "../../include/fedagg.h"
@@ -74,6 +75,7 @@ const RcclApi* api() {
 struct Comm {
   int n = 0;
   std::vector<ncclComm_t> comms;
+  std::vector<int> devs;  // device of comms[i]
 };
 
 int err(int code, const char* what, ncclResult_t r) {
@@ -96,6 +98,33 @@ int check(void* comm, int64_t count, const char* what, Comm** c) {
   if (!api()) return fa_internal_set_error(FA_E_HIP, "fa_rccl: RCCL could not be loaded");
   if (!comm || count < 0) return fa_internal_set_error(FA_E_ARG, what);
   *c = static_cast<Comm*>(comm);
+  return FA_OK;
+}
+
+// streams[i] must be a stream of device devs[i]: HIP would resolve a NULL stream against whatever device is
+// current when RCCL enqueues, so a group over several devices takes explicit per-device streams
+int check_streams(const Comm* c, void* const* streams, const char* what) {
+  char buf[256];
+  for (int i = 0; i < c->n; ++i) {
+    hipStream_t st = (hipStream_t)streams[i];
+    if (st == nullptr || st == hipStreamPerThread) {
+      if (c->n == 1) continue;
+      snprintf(buf, sizeof(buf), "%s: streams[%d] is NULL; a group over %d devices needs a stream per device", what,
+               i, c->n);
+      return fa_internal_set_error(FA_E_ARG, buf);
+    }
+    int d = -1;
+    if (hipStreamGetDevice(st, &d) != hipSuccess) {
+      (void)hipGetLastError();
+      snprintf(buf, sizeof(buf), "%s: streams[%d] is not a valid stream", what, i);
+      return fa_internal_set_error(FA_E_ARG, buf);
+    }
+    if (d != c->devs[i]) {
+      snprintf(buf, sizeof(buf), "%s: streams[%d] belongs to device %d, the communicator's rank %d is device %d",
+               what, i, d, i, c->devs[i]);
+      return fa_internal_set_error(FA_E_ARG, buf);
+    }
+  }
   return FA_OK;
 }
 
@@ -132,6 +161,7 @@ extern "C" int fa_rccl_init(int32_t ndev, const int32_t* devs, void** comm_out) 
   if (!c) return fa_internal_set_error(FA_E_HIP, "fa_rccl_init: out of memory");
   c->n = ndev;
   c->comms.resize(ndev);
+  c->devs.assign(devs, devs + ndev);
   std::vector<int> d(devs, devs + ndev);
   ncclResult_t r = a->init_all(c->comms.data(), ndev, d.data());
   if (r != ncclSuccess) {
@@ -165,6 +195,7 @@ extern "C" int fa_rccl_all_gather(void* comm, const void* const* send, void* con
   size_t sz;
   if ((e = dtype_of(dtype, &dt, &sz))) return e;
   if (!send || !recv || !streams) return fa_internal_set_error(FA_E_ARG, "fa_rccl_all_gather: NULL table");
+  if ((e = check_streams(c, streams, "fa_rccl_all_gather"))) return e;
   const RcclApi* a = api();
   return grouped(c, "fa_rccl_all_gather", [&](int i) {
     return a->all_gather(send[i], recv[i], (size_t)count, dt, c->comms[i], (hipStream_t)streams[i]);
@@ -180,6 +211,7 @@ extern "C" int fa_rccl_all_reduce(void* comm, const void* const* send, void* con
   size_t sz;
   if ((e = dtype_of(dtype, &dt, &sz))) return e;
   if (!send || !recv || !streams) return fa_internal_set_error(FA_E_ARG, "fa_rccl_all_reduce: NULL table");
+  if ((e = check_streams(c, streams, "fa_rccl_all_reduce"))) return e;
   const RcclApi* a = api();
   return grouped(c, "fa_rccl_all_reduce", [&](int i) {
     return a->all_reduce(send[i], recv[i], (size_t)count, dt, ncclSum, c->comms[i], (hipStream_t)streams[i]);
@@ -196,6 +228,7 @@ extern "C" int fa_rccl_gather(void* comm, const void* const* send, void* recv_ro
   if ((e = dtype_of(dtype, &dt, &sz))) return e;
   if (!send || !recv_root || !streams || root < 0 || root >= c->n)
     return fa_internal_set_error(FA_E_ARG, "fa_rccl_gather: bad root or NULL table");
+  if ((e = check_streams(c, streams, "fa_rccl_gather"))) return e;
   const RcclApi* a = api();
   return grouped(c, "fa_rccl_gather", [&](int i) {
     return a->gather(send[i], i == root ? recv_root : nullptr, (size_t)count, dt, root, c->comms[i],
@@ -213,6 +246,7 @@ extern "C" int fa_rccl_broadcast(void* comm, void* const* bufs, int64_t count, i
   if ((e = dtype_of(dtype, &dt, &sz))) return e;
   if (!bufs || !streams || root < 0 || root >= c->n)
     return fa_internal_set_error(FA_E_ARG, "fa_rccl_broadcast: bad root or NULL table");
+  if ((e = check_streams(c, streams, "fa_rccl_broadcast"))) return e;
   const RcclApi* a = api();
   return grouped(c, "fa_rccl_broadcast", [&](int i) {
     return a->broadcast(bufs[i], bufs[i], (size_t)count, dt, root, c->comms[i], (hipStream_t)streams[i]);

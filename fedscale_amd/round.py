@@ -15,6 +15,7 @@ epilogue (divide, fused FedYoGi, q-FedAvg hs + step) runs replicated on the summ
 """
 from __future__ import annotations
 
+import functools
 from typing import Optional
 
 import numpy as np
@@ -22,7 +23,7 @@ import torch
 
 from . import kernels as kx
 from .bucket import BucketLayout, ClientStaging
-from .state import ShardGroup
+from .state import DeviceStream, ShardGroup
 
 POLICIES = ("fedavg", "fedbuff", "qfedavg")
 
@@ -39,14 +40,36 @@ def default_capacity(layout: BucketLayout, K: int, device, budget_fraction: floa
     return cap
 
 
+def on_stream(fn):
+    """Run a method under ``self.dstream`` (its GPU and HIP stream current), unless that DeviceStream is
+    already the innermost one on this thread; without a dstream, on the caller's current stream."""
+
+    @functools.wraps(fn)
+    def run(self, *a, **k):
+        ds = self.dstream
+        if ds is None or DeviceStream.current() is ds:
+            return fn(self, *a, **k)
+        with ds:
+            return fn(self, *a, **k)
+
+    return run
+
+
 class DeviceRound:
     def __init__(self, layout: BucketLayout, device, K: int, policy: str, *, capacity: Optional[int] = None,
                  staging: Optional[ClientStaging] = None, last_f32: Optional[torch.Tensor] = None,
                  last_i64: Optional[torch.Tensor] = None, clients: Optional[ShardGroup] = None,
-                 mean_chain: bool = False):
+                 mean_chain: bool = False, dstream: Optional[DeviceStream] = None):
         """``mean_chain`` (q-FedAvg): fuse the plain FedAvg chain into the phase-1 kernel, so the round's
         mean (the reference's model_weights, aggregator.py:497-507) exists however many chunks the round
-        spans (fa_qfed_accumulate's ``chain``: +1 add per element, measured 9 % on the kernel)."""
+        spans (fa_qfed_accumulate's ``chain``: +1 add per element, measured 9 % on the kernel).
+        ``dstream``: the DeviceStream of the owning adapter; every kernel and copy of the round is issued on
+        it (None: the caller's current stream)."""
+        self.dstream = dstream
+        self._init(layout, device, K, policy, capacity, staging, last_f32, last_i64, clients, mean_chain)
+
+    @on_stream
+    def _init(self, layout, device, K, policy, capacity, staging, last_f32, last_i64, clients, mean_chain):
         if policy not in POLICIES:
             raise ValueError(f"policy {policy!r} not in {POLICIES}")
         if K < 1:
@@ -65,7 +88,7 @@ class DeviceRound:
             self.staging = staging
         else:
             cap = capacity or default_capacity(layout, K_local, self.device)
-            self.staging = ClientStaging(layout, self.device, min(cap, K_local))
+            self.staging = ClientStaging(layout, self.device, min(cap, K_local), dstream=self.dstream)
         self.cap = min(self.staging.capacity, capacity or self.staging.capacity)
         self.staging.generation += 1  # a new round takes the staging slots over
         self.generation = self.staging.generation
@@ -146,6 +169,7 @@ class DeviceRound:
         a64 = torch.from_numpy(self._w64[:n].copy()).to(self.device, non_blocking=True)
         return a32, a64
 
+    @on_stream
     def _fold_chunk(self):
         """Fold the staged chunk into the running state (not the last chunk of the round)."""
         self.staging.drain()
@@ -184,6 +208,7 @@ class DeviceRound:
         for t in tensors:
             self.cg.all_reduce_sum(t)
 
+    @on_stream
     def _finalize_mean_clients(self, denom32, denom64, out, cur_side, model_side, yogi):
         L = self.layout
         if self.slot:
@@ -200,6 +225,7 @@ class DeviceRound:
         kx.side_close(L.Q, mode, denom64, acc_i=self.acc_i, acc_d=self.acc_d, cur=cur_side, model=model_side)
 
     # ---- FedAvg / FedBuff: mean (+ optional fused FedYoGi) --------------------------------------
+    @on_stream
     def finalize_mean(self, denom32: float, denom64: float, *, out: torch.Tensor, cur_side: torch.Tensor,
                       model_side: Optional[torch.Tensor] = None, yogi: Optional[dict] = None):
         """Reduce the last chunk with the epilogue fused.
@@ -227,6 +253,7 @@ class DeviceRound:
         kx.side_accumulate(st.xi, n, L.Q, mode, w=a64, acc_i=self.acc_i, acc_d=self.acc_d, accumulate=not first)
         kx.side_close(L.Q, mode, denom64, acc_i=self.acc_i, acc_d=self.acc_d, cur=cur_side, model=model_side)
 
+    @on_stream
     def mean_from_staging(self, out: torch.Tensor, cur_side: torch.Tensor) -> bool:
         """The plain FedAvg mean of this round (aggregator.py:497-507), recomputed from the staged updates
         when they are all still resident (q-FedAvg rounds do not need it, but the reference keeps it in
@@ -249,6 +276,7 @@ class DeviceRound:
         return True
 
     # ---- q-FedAvg --------------------------------------------------------------------------------
+    @on_stream
     def finalize_qfed(self, *, out: torch.Tensor, model_side: torch.Tensor, sqnorm_allreduce=None):
         """Fold the last chunk, then hs (optimizers.py:96-98) and new = L - delta/(hs+1e-10) (:101-104).
 
@@ -259,6 +287,7 @@ class DeviceRound:
             sqnorm_allreduce(self.sqnorm)
         self.qfed_finish(out=out, model_side=model_side)
 
+    @on_stream
     def qfed_fold(self):
         """Phase 1 of the finish: fold the last chunk.  ``sqnorm`` then holds this shard's partial per-client
         squared norms (the fp32 bucket part; summed over the shards by the caller between the phases)."""
@@ -270,6 +299,7 @@ class DeviceRound:
             # delta and delta_s are per-rank partial chains
             self._cross_rank_sum(self.delta, self.delta_s, self.sqnorm, self.sqnorm_side)
 
+    @on_stream
     def qfed_finish(self, *, out: torch.Tensor, model_side: torch.Tensor):
         """Phase 2: hs over the (shard-summed) norms and the step."""
         L = self.layout

@@ -23,7 +23,7 @@ benchmark and tests), with two ways to spread a round over the ranks (SURVEY §8
 from __future__ import annotations
 
 import atexit
-import sys
+import threading
 import weakref
 from dataclasses import dataclass
 from typing import Optional
@@ -31,6 +31,91 @@ from typing import Optional
 import torch
 
 from .bucket import BucketLayout
+
+
+class DeviceStream:
+    """A GPU and the HIP stream an adapter (or one part of a sharded adapter) issues ALL its work on.
+
+    ``with ds:`` makes the GPU current and the stream current on it, for torch ops and for the library
+    (``kernels._stream`` passes the current stream of the tensor's device), and restores both on exit.  So
+    one host thread drives several GPUs and every launch, copy and event of a part lands on the part's own
+    device, whatever device the caller had current (the null stream would resolve against the caller's
+    current device).  Work the adapter does not own — device tensors handed in by the caller — is ordered
+    by ``wait_caller()``: the stream waits for the stream that was current on this device at entry."""
+
+    __slots__ = ("device", "index", "stream", "handle")
+    _tls = threading.local()
+
+    def __init__(self, device, stream: "Optional[torch.cuda.Stream]" = None):
+        d = torch.device(device) if not isinstance(device, int) else torch.device("cuda", device)
+        if d.type != "cuda":
+            raise ValueError(f"device {d}: the aggregation path runs on the GPU only (no CPU fallback)")
+        if d.index is None:
+            d = torch.device("cuda", torch.cuda.current_device())
+        self.device, self.index = d, d.index
+        self.stream = stream if stream is not None else torch.cuda.Stream(device=d)
+        self.handle = self.stream.cuda_stream  # never 0: a stream of this device, not the null stream
+
+    @classmethod
+    def current(cls) -> "Optional[DeviceStream]":
+        """The innermost DeviceStream entered on this thread (None outside any)."""
+        st = getattr(cls._tls, "stack", None)
+        return st[-1][0] if st else None
+
+    def __enter__(self):
+        st = getattr(self._tls, "stack", None)
+        if st is None:
+            st = self._tls.stack = []
+        prev_dev = torch.cuda.current_device()
+        if prev_dev != self.index:
+            torch.cuda.set_device(self.index)
+        prev = torch.cuda.current_stream(self.index)  # the caller's stream on this device
+        torch.cuda.set_stream(self.stream)
+        st.append((self, prev_dev, prev))
+        return self
+
+    def __exit__(self, *exc):
+        return self._exit(False)
+
+    def _exit(self, join: bool):
+        _, prev_dev, prev = self._tls.stack.pop()
+        if join and prev != self.stream:
+            prev.wait_stream(self.stream)  # no host sync: the caller's stream is ordered after our work
+        torch.cuda.set_stream(prev)
+        if prev_dev != self.index:
+            torch.cuda.set_device(prev_dev)
+        return False
+
+    def joined(self) -> "_Joined":
+        """Like ``with ds:``, and on exit the caller's stream on this device waits for everything issued
+        inside (an event, no host sync): an adapter's public calls keep the ordering a caller on its own
+        stream expects (device buffers it reads afterwards are written), while the work itself runs on
+        ``stream``."""
+        return _Joined(self)
+
+    def wait_caller(self):
+        """Order this stream after the work the caller queued on this device before its outermost entry."""
+        for ds, _, prev in getattr(self._tls, "stack", None) or ():
+            if ds is self:
+                if prev != self.stream:
+                    self.stream.wait_stream(prev)
+                return
+        cur = torch.cuda.current_stream(self.index)
+        if cur != self.stream:
+            self.stream.wait_stream(cur)
+
+
+class _Joined:
+    __slots__ = ("ds",)
+
+    def __init__(self, ds: DeviceStream):
+        self.ds = ds
+
+    def __enter__(self):
+        return self.ds.__enter__()
+
+    def __exit__(self, *exc):
+        return self.ds._exit(True)
 
 
 @dataclass
@@ -169,7 +254,10 @@ def _close_live_groups():
             pass
 
 
-_LIVE_GROUPS: "weakref.WeakSet" = weakref.WeakSet()
+#: groups with an open RCCL communicator, held STRONGLY until closed: a communicator is destroyed only by an
+#: explicit close() or by the exit hook below (while the HIP runtime is still up) — never from a GC
+#: finalizer, which may run on any thread, gRPC servicer threads included
+_LIVE_GROUPS: "set" = set()
 atexit.register(_close_live_groups)
 
 
@@ -180,6 +268,12 @@ class DeviceGroup:
     than once (several shards on one card, as in tests) or RCCL is unavailable, the same steps run as
     device-to-device copies.  Either way the combination order is fixed (all-gather, then a fixed-order
     sum), so the result does not depend on the transport.
+
+    Position i of the group owns ``streams[i]``, a ``DeviceStream`` of ``devices[i]``: the part of a
+    ``ShardedModelAdapter`` at that position issues all its work on it, and the group's collectives run on
+    it (RCCL gets one explicit stream per device, never the null stream).  A collective first orders each
+    position's stream after the caller's current stream on that device and, at the end, the caller's
+    current streams after the group's, so plain tensors handed in and read back need no extra sync.
 
     ``transport``: "rccl", "copy" or None (choose: RCCL whenever the devices are distinct)."""
 
@@ -202,6 +296,7 @@ class DeviceGroup:
         if transport == "rccl" and not distinct:
             raise ValueError("RCCL needs one shard per GPU (a device appears twice)")
         self.transport = transport
+        self.streams = [DeviceStream(d) for d in devs]
         self._comm = None
 
     # ---- RCCL communicator ------------------------------------------------------------------------
@@ -215,7 +310,7 @@ class DeviceGroup:
             h = ctypes.c_void_p()
             _native.call("fa_rccl_init", self.world, devs, ctypes.byref(h))
             self._comm = h
-            _LIVE_GROUPS.add(self)  # destroyed at interpreter exit while the HIP runtime is still up
+            _LIVE_GROUPS.add(self)  # destroyed by close() or at interpreter exit, never by GC
         return self._comm
 
     def close(self):
@@ -226,13 +321,9 @@ class DeviceGroup:
             _LIVE_GROUPS.discard(self)
             _native.call("fa_rccl_destroy", comm)
 
-    def __del__(self):
-        try:
-            if sys.is_finalizing():  # too late to call into RCCL safely; _close_live_groups ran at exit
-                return
-            self.close()
-        except Exception:
-            pass
+    def stream_handles(self) -> list:
+        """The hipStream_t of every position (what the fa_rccl_* stream tables hold)."""
+        return [ds.handle for ds in self.streams]
 
     def _tables(self, *lists):
         import ctypes
@@ -240,7 +331,7 @@ class DeviceGroup:
         out = []
         for lst in lists:
             out.append((ctypes.c_void_p * self.world)(*[None if t is None else t.data_ptr() for t in lst]))
-        streams = (ctypes.c_void_p * self.world)(*[torch.cuda.current_stream(d).cuda_stream for d in self.devices])
+        streams = (ctypes.c_void_p * self.world)(*self.stream_handles())
         return out, streams
 
     @staticmethod
@@ -250,24 +341,63 @@ class DeviceGroup:
         return {torch.float32: _native.FA_DT_F32, torch.float64: _native.FA_DT_F64,
                 torch.int64: _native.FA_DT_I64}[t.dtype]
 
+    def _enter(self):
+        """Every position's stream waits for the caller's current stream on its device."""
+        for ds in self.streams:
+            cur = torch.cuda.current_stream(ds.index)
+            if cur != ds.stream:
+                ds.stream.wait_stream(cur)
+
+    def _leave(self):
+        """The caller's current streams wait for the group's work."""
+        for ds in self.streams:
+            cur = torch.cuda.current_stream(ds.index)
+            if cur != ds.stream:
+                cur.wait_stream(ds.stream)
+
+    def _barrier(self):
+        """Every position's stream waits for what every position has queued so far (copy transport: a copy
+        reads another position's buffer, so both sides must be ordered)."""
+        evs = []
+        for ds in self.streams:
+            ev = torch.cuda.Event()
+            ev.record(ds.stream)
+            evs.append(ev)
+        for ds in self.streams:
+            for ev in evs:
+                ds.stream.wait_event(ev)
+
+    def _copy_each(self, fn):
+        """Run fn(i) under position i's DeviceStream for every i, between two barriers."""
+        self._barrier()
+        for i, ds in enumerate(self.streams):
+            with ds:
+                fn(i)
+        self._barrier()
+
     # ---- collectives over the parts ---------------------------------------------------------------
     def all_gather(self, parts, outs):
         """outs[i][r*n:(r+1)*n] = parts[r] for every part i (n = parts[r].numel(), equal for all r)."""
         n = parts[0].numel()
+        self._enter()
         if self.transport == "rccl":
             from . import _native
 
             (send, recv), streams = self._tables(parts, outs)
             _native.call("fa_rccl_all_gather", self._rccl(), send, recv, n, self._dt(parts[0]), streams)
-            return outs
-        for i, o in enumerate(outs):
-            for r, p in enumerate(parts):
-                o[r * n:(r + 1) * n].copy_(p.reshape(-1), non_blocking=True)
+        else:
+            def copy(i):
+                for r, p in enumerate(parts):
+                    outs[i][r * n:(r + 1) * n].copy_(p.reshape(-1), non_blocking=True)
+
+            self._copy_each(copy)
+        self._leave()
         return outs
 
     def gather(self, parts, out_root, root: int = 0):
         """out_root[r*n:(r+1)*n] = parts[r], on device ``root``."""
         n = parts[0].numel()
+        self._enter()
         if self.transport == "rccl":
             import ctypes
 
@@ -276,33 +406,50 @@ class DeviceGroup:
             (send,), streams = self._tables(parts)
             _native.call("fa_rccl_gather", self._rccl(), send, ctypes.c_void_p(out_root.data_ptr()), n,
                          self._dt(parts[0]), root, streams)
-            return out_root
-        for r, p in enumerate(parts):
-            out_root[r * n:(r + 1) * n].copy_(p.reshape(-1), non_blocking=True)
+        else:
+            def copy(i):
+                if i == root:
+                    for r, p in enumerate(parts):
+                        out_root[r * n:(r + 1) * n].copy_(p.reshape(-1), non_blocking=True)
+
+            self._copy_each(copy)
+        self._leave()
         return out_root
 
     def broadcast(self, bufs, root: int = 0):
         """bufs[i] <- bufs[root] for every part i."""
         n = bufs[root].numel()
+        self._enter()
         if self.transport == "rccl":
             from . import _native
 
             (b,), streams = self._tables(bufs)
             _native.call("fa_rccl_broadcast", self._rccl(), b, n, self._dt(bufs[root]), root, streams)
-            return bufs
-        for i, t in enumerate(bufs):
-            if i != root:
-                t.copy_(bufs[root], non_blocking=True)
+        else:
+            def copy(i):
+                if i != root:
+                    bufs[i].copy_(bufs[root], non_blocking=True)
+
+            self._copy_each(copy)
+        self._leave()
         return bufs
 
     def sum_f64(self, parts, scratch=None):
         """parts[i] <- ((parts[0] + parts[1]) + ...) on every device: per-shard fp64 partials (q-FedAvg's
-        per-client squared norms), combined by an all-gather and a fixed-order sum (fa_sum_rows_f64)."""
+        per-client squared norms), combined by an all-gather and a fixed-order sum (fa_sum_rows_f64), each
+        position's sum on its own stream."""
         from . import kernels as kx
 
         n = parts[0].numel()
-        outs = scratch or [torch.empty(self.world * n, dtype=torch.float64, device=p.device) for p in parts]
-        self.all_gather(parts, outs)
-        for p, o in zip(parts, outs):
-            kx.sum_rows_f64(o.view(self.world, n), p)
+        if scratch is None:
+            scratch = []
+            for ds in self.streams:
+                with ds:  # allocated on the stream that uses it (the caching allocator reuses per stream)
+                    scratch.append(torch.empty(self.world * n, dtype=torch.float64, device=ds.device))
+        self.all_gather(parts, scratch)
+        self._enter()
+        for ds, p, o in zip(self.streams, parts, scratch):
+            with ds:
+                kx.sum_rows_f64(o.view(self.world, n), p)
+        self._leave()
         return parts

@@ -10,8 +10,13 @@
  *   - return 0 on success, a negative FA_E* code on failure; fa_last_error_string() describes the
  *     last failure of the calling thread.  No exception crosses the ABI.
  *   - every pointer is DEVICE memory owned by the caller (16-byte aligned); every launch is
- *     asynchronous on the caller's `stream` (a hipStream_t; NULL = the legacy default stream) with no
- *     implicit synchronisation.  Functions are stateless and reentrant.
+ *     asynchronous on the caller's `stream` (a hipStream_t) with no implicit synchronisation.
+ *     Functions are stateless and reentrant.
+ *   - the device: a call's work runs on the GPU that holds its output.  A non-NULL `stream` must be a
+ *     stream of that GPU (else FA_E_ARG, nothing launched); NULL means the legacy default stream of THAT
+ *     GPU — the library makes it current for the call and restores the caller's current device after, so
+ *     one host thread can drive several GPUs (fedscale_amd/csrc/fa_device.h).  Launch plans size their
+ *     grids by that GPU's CU count.
  *   - a "bucket" is the fp32 tensors of a state_dict concatenated in state_dict order: P elements,
  *     padded with zeros to a row stride `ld` (multiple of 64).  Client updates live client-major,
  *     x[k*ld + p].  Every per-column buffer (acc, out, last, m, v, delta) holds >= round_up(P, 4)
@@ -225,7 +230,9 @@ int fa_sum_rows_f64(const double* x, int64_t ld, int32_t n, int64_t K, double* o
  * loaded is reused); fa_rccl_available() == 0 when it cannot be found.
  *
  * Tables (send / recv / bufs / streams) are HOST arrays of N device pointers / hipStream_t, indexed by
- * the position in `devs` given to fa_rccl_init.  count is in elements of `dtype` per device.
+ * the position in `devs` given to fa_rccl_init.  count is in elements of `dtype` per device.  streams[i]
+ * must be a stream of devs[i] (FA_E_ARG otherwise, nothing enqueued); NULL is accepted only by a one-device
+ * communicator.
  *   fa_rccl_init       ncclCommInitAll over devs[0..ndev) (distinct device ordinals)
  *   fa_rccl_all_gather recv[i][r*count + j] = send[r][j]
  *   fa_rccl_all_reduce recv[i][j] = sum_r send[r][j]

@@ -115,6 +115,111 @@ def test_sharded_equals_single_gpu(gpu_device, name):
         assert_state_equal(list(aggs[0].model_weights), list(aggs[1].model_weights), f"{name} mean r{r}")
 
 
+#: entry points that enqueue GPU work (their last argument is the stream, or the per-device stream table)
+LAUNCHES = {"fa_reduce", "fa_reduce_yogi", "fa_yogi_step", "fa_qfed_accumulate", "fa_qfed_hs", "fa_qfed_finalize",
+            "fa_sum_rows_f64", "fa_side_accumulate", "fa_side_close", "fa_side_yogi", "fa_side_qfed_accumulate",
+            "fa_side_qfed_finalize", "fa_fill_synthetic", "fa_prefix_box_combine", "fa_rccl_all_gather",
+            "fa_rccl_all_reduce", "fa_rccl_gather", "fa_rccl_broadcast"}
+
+
+def _spy_native(monkeypatch):
+    """Record (entry point, stream argument, innermost DeviceStream) of every native call."""
+    from fedscale_amd import _native
+    from fedscale_amd import kernels as kx
+    from fedscale_amd.state import DeviceStream
+
+    calls, real = [], _native.call
+
+    def spy(fn, *args):
+        calls.append((fn, args[-1] if args else None, DeviceStream.current()))
+        return real(fn, *args)
+
+    monkeypatch.setattr(_native, "call", spy)
+    monkeypatch.setattr(kx, "call", spy)
+    return calls
+
+
+def _check_part_streams(calls, adapter, ctx):
+    streams = {ds.handle: ds for ds in adapter.group.streams} if hasattr(adapter, "group") else {
+        adapter.dstream.handle: adapter.dstream}
+    launches = [c for c in calls if c[0] in LAUNCHES]
+    assert launches, ctx
+    for fn, st, cur in launches:
+        if fn.startswith("fa_rccl_"):
+            hs = list(st)
+            assert hs == adapter.group.stream_handles() and all(hs), f"{ctx}: {fn} stream table {hs}"
+            continue
+        assert st, f"{ctx}: {fn} launched on the null stream"
+        assert cur is not None, f"{ctx}: {fn} issued outside any part's DeviceStream"
+        assert st == cur.handle, f"{ctx}: {fn} on stream {st:#x}, its part's stream is {cur.handle:#x}"
+        assert st in streams and streams[st] is cur, f"{ctx}: {fn} on a stream no part of this adapter owns"
+    return launches
+
+
+@pytest.mark.parametrize("sharding", list(SHARDINGS))
+@pytest.mark.parametrize("name", ["fedavg_wide_k64", "fedbuff_k8", "fedyogi_wide_3rounds", "qfedavg_q1_lrdecay"])
+def test_every_native_call_runs_on_its_parts_stream(gpu_device, monkeypatch, name, sharding):
+    """Every kernel launch and collective of a sharded round carries the non-null stream of the part whose
+    buffers it touches (its own GPU's stream; the null stream would resolve against whatever device the
+    calling thread has current), with chunk folds (capacity 2), every server step and egress; the results
+    stay bit-exact / within tolerance of the reference fixtures."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator, DeviceAsyncAggregator
+
+    sc = Scenario(name)
+    devices, transport = SHARDINGS[sharding]
+    args, opt, adapter = _sharded(sc, devices, transport, capacity=2)
+    calls = _spy_native(monkeypatch)
+    if sc.meta["policy"] == "fedbuff":
+        agg = DeviceAsyncAggregator(adapter, args)
+        agg.round = sc.meta["round"]
+        for k, s in enumerate(sc.meta["staleness"]):
+            agg.client_task_model_version[101 + k] = agg.round - s
+    else:
+        agg = DeviceAggregator(adapter, args)
+    for r, ks in sc.rounds():
+        if sc.meta["policy"] == "q-fedavg":
+            args.learning_rate = sc.meta["lrs"][r]
+        agg.start_round(len(ks))
+        for res in sc.results(ks, r):
+            agg.on_result(res)
+        _check(sc, r, adapter.get_weights(), adapter, f"{name} {sharding} r{r}")
+        list(agg.model_weights)  # the FedAvg mean's D2H runs on the parts' streams too
+    launches = _check_part_streams(calls, adapter, f"{name} {sharding}")
+    used = {c[1] for c in launches if not c[0].startswith("fa_rccl_")}
+    assert used == set(adapter.group.stream_handles()), "every part launched on its own stream"
+    if sc.meta["policy"] == "q-fedavg":
+        assert any(c[0] in ("fa_rccl_all_gather", "fa_sum_rows_f64") for c in launches)
+    adapter.group.close()
+
+
+def test_single_adapter_runs_on_its_own_stream(gpu_device, monkeypatch):
+    """The single-GPU adapter too: every launch on its DeviceStream (never the null stream), and the caller's
+    stream is ordered after each call (a device buffer read right after a round on the default stream sees
+    the round's result)."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    sc = Scenario("fedyogi_wide_3rounds")
+    args = sc.args()
+    single = TorchModelAdapter(StateDictModule(sc.names, sc.init_state()),
+                               optimizer=TorchServerOptimizer(args.gradient_policy, args, "cuda:0"), device="cuda:0",
+                               staging_capacity=3)
+    calls = _spy_native(monkeypatch)
+    agg = DeviceAggregator(single, args)
+    for r, ks in sc.rounds():
+        agg.start_round(len(ks))
+        for res in sc.results(ks, r):
+            agg.on_result(res)
+        cur = single._f[single._cur][:single.layout.P].cpu()  # default stream, no explicit sync
+        got = single.get_weights()  # synchronises with the round's event
+        flat = torch.cat([w.reshape(-1) for w, e in zip(got, single.layout.entries) if e.kind == "f"])
+        assert torch.equal(cur, flat), f"round {r}: the caller's stream was not ordered after the round"
+        assert_state_close(got, sc.expected(r), YOGI_RTOL, f"round {r}")
+    launches = [c for c in calls if c[0] in LAUNCHES]
+    assert launches and all(c[1] == single.dstream.handle and c[2] is single.dstream for c in launches)
+
+
 def _executor_payload(res):
     return pickle.dumps(res)
 
