@@ -221,21 +221,38 @@ def _c1_updates(seed: int, K: int):
     return names, shapes, base, ups
 
 
+C1_JOB_CONF = os.path.join(ROOT, "tests", "golden", "c1_femnist_job_conf.json")
+
+
+def c1_job_conf() -> dict:
+    """Config 1's flags: benchmark/configs/femnist/conf.yml's job_conf converted as docker/driver.py:81-95 and
+    parsed by config_parser.py, num_participants 50 -> 10 (tests/golden/gen_golden_r3.py, from the reference)."""
+    with open(C1_JOB_CONF) as f:
+        return json.load(f)
+
+
 def c1_host_round(dev, seed: int, rounds: int = 50) -> dict:
-    """BASELINE config 1 (FEMNIST small-CNN, K = 10) through the drop-in: start_round, K on_result calls
-    with host dicts (pinned staging + H2D), the fused reduce, and get_weights() (D2H) — the whole round
-    the reference runs on the CPU (aggregator.py:489-511, torch_model_adapter.py:23-47)."""
+    """BASELINE config 1 (FEMNIST small-CNN, K = num_participants of the job config = 10) through the drop-in:
+    start_round, K on_result calls with host dicts (pinned staging + H2D), the fused reduce, and get_weights()
+    (D2H) — the whole round the reference runs on the CPU (aggregator.py:489-511, torch_model_adapter.py:23-47)."""
+    import argparse
+
     import numpy as np
     import torch
 
     from fedscale_amd import synth
     from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
     from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
 
-    K = 10
+    job = c1_job_conf()
+    args = argparse.Namespace(**job["args"])
+    K = args.num_participants
     names, shapes, base, ups = _c1_updates(seed, K)
     model = synth.LayoutModule(names, shapes, [torch.float32] * len(names))
-    agg = DeviceAggregator(TorchModelAdapter(model, device=dev))
+    on = args.cuda_device or dev  # aggregator.py:47: --cuda_device, else the current GPU
+    agg = DeviceAggregator(TorchModelAdapter(model, optimizer=TorchServerOptimizer(args.gradient_policy, args, on),
+                                             device=on), args)
     ts = []
     for r in range(rounds + 5):
         torch.cuda.synchronize(dev)
@@ -248,6 +265,10 @@ def c1_host_round(dev, seed: int, rounds: int = 50) -> dict:
     ms = float(np.median(ts[5:])) * 1e3
     return {"clients": K, "params": sum(int(np.prod(s)) for s in shapes), "round_ms_incl_h2d_d2h": ms,
             "client_updates_per_s": K / (ms * 1e-3),
+            "job_config": {"file": "benchmark/configs/femnist/conf.yml (job_conf)",
+                           "num_participants": f"{job['job_conf_num_participants']} -> {K}",
+                           "gradient_policy": args.gradient_policy, "learning_rate": args.learning_rate,
+                           "local_steps": args.local_steps, "data_set": args.data_set},
             "note": "host dicts in, global model out (get_weights); median of %d rounds" % rounds}
 
 
@@ -257,7 +278,7 @@ def cpu_baseline_c1(seed: int, rounds: int = 50) -> dict:
 
     from oracle.cpu_reference import fedavg_close, fedavg_step
 
-    K = 10
+    K = c1_job_conf()["args"]["num_participants"]
     _, _, _, ups = _c1_updates(seed, K)
     ts = []
     for r in range(rounds + 5):
@@ -311,7 +332,10 @@ class Workload:
     device path's chunk folding does."""
 
     def __init__(self, policy, K, P_total, rank, world, dev, seed, shards, *, weak=False, chunk=None,
-                 budget_fraction=0.6, sets=1):
+                 budget_fraction=0.6, sets=1, mean_chain="auto"):
+        """``mean_chain`` (q-FedAvg): carry the plain FedAvg chain in the phase-1 kernel (fa_qfed_accumulate's
+        ``chain``, the reference's model_weights, aggregator.py:497-507).  "auto" does what the drop-in does:
+        fuse it whenever the round spans several resident chunks (DeviceRound, device_keep_mean=True)."""
         import numpy as np
         import torch
 
@@ -336,6 +360,7 @@ class Workload:
             cap = min(cap, kx.qfed_max_chunk())
         self.C = min(K, cap, chunk or K)
         self.passes = [(k0, min(self.C, K - k0)) for k0 in range(0, K, self.C)]
+        self.mean_chain = (len(self.passes) > 1) if mean_chain == "auto" else bool(mean_chain)
         self.xs = []
         for i in range(sets):  # sets > 1: rotate input sets so the 256 MiB Infinity Cache cannot serve repeats
             x = torch.empty(self.C, ld, dtype=torch.float32, device=dev)
@@ -375,12 +400,20 @@ class Workload:
                                            device=dev))
             synth.fill(self.qf["last"], 1, self.P, seed=seed + (0 if self.cmode else 7919 * rank), scale_noise=0.0)
             self.qf["last"] = self.qf["last"][0]
+            self.qf["chain"] = torch.zeros(ld, device=dev) if (self.mean_chain and not self.cmode) else None
         self.stream = torch.cuda.current_stream(dev)
 
     @property
     def alg_bytes(self) -> int:
-        """SURVEY §8d algorithmic bytes of this rank's dominant kernel(s) per round."""
-        return 4 * self.K * self.P + 4 * self.P + EXTRA_BYTES[self.policy](self.K, self.P)
+        """SURVEY §8d algorithmic bytes of this rank's dominant kernel(s) per round.  q-FedAvg over several
+        passes re-reads last and reads back delta (and the chain) on every pass after the first."""
+        b = 4 * self.K * self.P + 4 * self.P + EXTRA_BYTES[self.policy](self.K, self.P)
+        if self.policy == "qfedavg":
+            n = len(self.passes)
+            b += 12 * self.P * (n - 1)  # passes 2..n: last re-read, delta read back and written again
+            if self.qf is not None and self.qf["chain"] is not None:
+                b += 4 * self.P * (2 * n - 1)  # chain written every pass, read back on passes 2..n
+        return b
 
     def step(self, ev=None):
         from fedscale_amd import kernels as kx
@@ -397,7 +430,7 @@ class Workload:
             for i, (k0, n) in enumerate(self.passes):
                 kx.qfed_accumulate(x, n, P, last=qf["last"], alpha=qf["alpha"][k0:k0 + n], lr=qf["lr"],
                                    delta=qf["delta"], sqnorm=qf["sq"][kb + k0:kb + k0 + n], workspace=qf["ws"],
-                                   accumulate=i > 0)
+                                   accumulate=i > 0, chain=qf["chain"])
             if ev is not None:
                 ev[1].record(st)
             if self.cmode:  # per-rank partial delta chains + each client's norm from its owner rank
@@ -458,6 +491,21 @@ def _max_over_ranks(vals, dev, world, backend):
     return [float(v) for v in t.cpu()]
 
 
+def _all_ranks(val: float, dev, world, backend) -> list:
+    """[value of rank 0, rank 1, ...] (an all-gather of one float per rank)."""
+    import torch
+    import torch.distributed as dist
+
+    if world == 1:
+        return [float(val)]
+    t = torch.tensor([float(val)], dtype=torch.float64)
+    if backend == "nccl":
+        t = t.to(dev)
+    out = [torch.zeros_like(t) for _ in range(world)]
+    dist.all_gather(out, t)
+    return [float(o.cpu()[0]) for o in out]
+
+
 def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend):
     """Warmup, then exactly ``steps`` rounds between barrier + synchronize; (wall s, mean dominant-kernel
     ms), both max over ranks."""
@@ -474,7 +522,7 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend):
     _sync_all(dev, world)
     wall = time.perf_counter() - t0
     kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
-    return _max_over_ranks([wall, kern_ms], dev, world, backend), kern_ms
+    return _max_over_ranks([wall, kern_ms], dev, world, backend), kern_ms, _all_ranks(kern_ms, dev, world, backend)
 
 
 MEM_FRACTION = 0.6
@@ -484,13 +532,28 @@ def config_line(name, cfg, dev, rank, world, shards, seed, backend, steps=5, war
     """A BASELINE config on all ranks (parameter-sharded over them), for other_configs."""
     kw.setdefault("budget_fraction", MEM_FRACTION)
     w = Workload(cfg["policy"], cfg["clients"], cfg["params"], rank, world, dev, seed, shards, **kw)
-    (wall, kern_max), _ = time_workload(w, steps, warmup, dev, world, backend)
+    (wall, kern_max), _, _ = time_workload(w, steps, warmup, dev, world, backend)
     ms = wall * 1e3 / steps
     out = {"policy": cfg["policy"], "clients": cfg["clients"], "params": cfg["params"], "n_gpus": world,
            "params_per_gpu": w.P, "resident_clients": w.C, "passes": len(w.passes), "round_ms": ms,
            "client_updates_per_s": cfg["clients"] / (ms * 1e-3),
            "hbm_gbps_per_gpu": w.alg_bytes / (ms * 1e-3) / 1e9, "dominant_kernel_ms": kern_max,
            "hbm_gbps_kernel": w.alg_bytes / (kern_max * 1e-3) / 1e9}
+    if cfg["policy"] == "qfedavg":
+        out["mean_chain"] = w.mean_chain
+        if w.mean_chain:
+            out["mean_chain_note"] = ("timed as the drop-in runs this round: it spans several chunks, so the FedAvg "
+                                      "chain (the reference's model_weights) is fused into phase 1; the chain-free "
+                                      "kernel is beside it (no_chain)")
+            w.free()
+            kw2 = dict(kw, mean_chain=False)
+            w2 = Workload(cfg["policy"], cfg["clients"], cfg["params"], rank, world, dev, seed, shards, **kw2)
+            (wall2, kern2), _, _ = time_workload(w2, steps, warmup, dev, world, backend)
+            ms2 = wall2 * 1e3 / steps
+            out["no_chain"] = {"round_ms": ms2, "dominant_kernel_ms": kern2,
+                               "hbm_gbps_kernel": w2.alg_bytes / (kern2 * 1e-3) / 1e9,
+                               "chain_cost_pct": 100.0 * (kern_max / kern2 - 1.0)}
+            w = w2
     if len(w.passes) > 1:
         out["note"] = ("K > resident chunk: each round streams %d passes over the resident %d clients (every pass "
                        "reads its 4*C*P bytes from HBM; the ingress refill is not part of this device rate)"
@@ -553,7 +616,9 @@ def main():
     global MEM_FRACTION
     MEM_FRACTION = args.mem_fraction
     w = Workload(policy, K, P, rank, world, dev, args.seed, shards, weak=weak, budget_fraction=args.mem_fraction)
-    (wall, kern_ms_max), kern_ms = time_workload(w, args.steps, args.warmup, dev, world, args.dist_backend)
+    (wall, kern_ms_max), kern_ms, kern_ms_ranks = time_workload(w, args.steps, args.warmup, dev, world,
+                                                                 args.dist_backend)
+    pg_world = dist.get_world_size() if world > 1 else 1
     strong = not weak and not w.cmode
 
     reassembly_ms = None
@@ -592,7 +657,9 @@ def main():
     if rank == 0:
         ms_per_step = wall * 1e3 / args.steps
         value = (K if strong else world * K) * args.steps / wall
-        achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+        # the slowest rank's kernel sets the job's pace: roofline from the max over ranks (rank 0's slice is the
+        # largest, so bytes / max time is the conservative per-GPU rate); N = 1: the same number
+        achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
         traffic = None
         if os.path.exists(PMC_FILE):
             try:
@@ -627,7 +694,7 @@ def main():
             "data": "synthetic full-weight client updates (base + noise, hash-generated on device), HBM-resident",
             "config": config,
             "hbm_gbps": achieved,
-            "kernel_ms": kern_ms,
+            "kernel_ms": kern_ms_max,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": ("k_qfed_accum + k_qfed_gather (fa_qfed_accumulate)" if policy == "qfedavg"
@@ -636,8 +703,13 @@ def main():
                                      "fedbuff": "k_reduce weighted (fa_reduce FA_FINALIZE)",
                                      "fedyogi": "k_reduce EPI_YOGI (fa_reduce_yogi)"}[policy]),
                          "alg_bytes_per_launch": alg_bytes / launches, "launches_per_step": launches,
-                         "kernel_ms_per_launch": kern_ms / launches},
+                         "kernel_ms_per_launch": kern_ms_max / launches},
         }
+        if world > 1:  # self-checking SCALE records: every rank's kernel time and the process group's size
+            res["ranks"] = {"world_process_group": pg_world, "backend": args.dist_backend,
+                            "kernel_ms_per_rank": kern_ms_ranks, "kernel_ms_max": kern_ms_max,
+                            "kernel_ms_rank0": kern_ms,
+                            "roofline_from": "max over ranks of the dominant kernel's mean time per step"}
         if reassembly_ms is not None:
             res["reassembly_ms"] = reassembly_ms
         if other is not None:

@@ -20,7 +20,8 @@ DEFAULT_ARGS = dict(gradient_policy=None, learning_rate=0.05, min_learning_rate=
 def scenario_names(kind="single"):
     """kind 'single': one global model per scenario; 'cohorts': Auxo multi-cohort scenarios; 'heterofl';
     'client': FedProx / local-DP client-side fixtures."""
-    names = sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "*.json")))
+    names = sorted(os.path.basename(p)[:-5] for p in glob.glob(os.path.join(GOLDEN, "*.json"))
+                   if os.path.exists(p[:-5] + ".npz"))  # (c1_femnist_job_conf.json is a config, not a scenario)
     if kind == "client":  # client-side handler fixtures (gen_golden_client.py)
         return [n for n in names if n.startswith("client_")]
     names = [n for n in names if not n.startswith("client_")]
@@ -67,9 +68,14 @@ class Scenario:
     def yogi_state(self, r):
         return self._tensors(f"yogi_m/{r}"), self._tensors(f"yogi_v/{r}")
 
+    def _client_tensors(self, k):
+        if f"client/{k}/0" in self.arrays:
+            return self._tensors(f"client/{k}")
+        return [self.arrays[f"clients/{i}"][k] for i in range(self.T)]  # stacked [K, ...] per tensor
+
     def client(self, k):
         vals = []
-        for a in self._tensors(f"client/{k}"):
+        for a in self._client_tensors(k):
             vals.append(a.astype(np.float32) if a.dtype == np.float16 else a)
         every = self.meta.get("dict_every")
         if every and k % every == 0:
@@ -162,3 +168,14 @@ class ClientScenario:
 
     def list(self, prefix, n):
         return [self.arrays[f"{prefix}/{i}"] for i in range(n)]
+
+
+def c1_job_args():
+    """Config 1's aggregator flags: benchmark/configs/femnist/conf.yml's job_conf as the reference launcher
+    converts it (docker/driver.py:81-95) and config_parser.py parses it, num_participants overridden to 10
+    (tests/golden/gen_golden_r3.py wrote them from the real reference)."""
+    with open(os.path.join(GOLDEN, "c1_femnist_job_conf.json")) as f:
+        doc = json.load(f)
+    a = dict(DEFAULT_ARGS)
+    a.update(doc["args"])
+    return argparse.Namespace(**a), doc
