@@ -170,6 +170,7 @@ class TorchModelAdapter(ModelAdapterBase):
         self._egress_cache = None
         self._egress_id = next(_EGRESS_IDS)
         self._module_version = 0 if module_in_sync else -1
+        self._egress_ds: Optional[DeviceStream] = None  # D2H stream of egress (made on first use)
 
     # ---- internal buffers ---------------------------------------------------------------------
     def _snapshot(self) -> FlatState:
@@ -231,15 +232,19 @@ class TorchModelAdapter(ModelAdapterBase):
         lock, so no round commits meanwhile; synchronous).  Parameter-sharded SPMD ranks all-gather
         first: every rank must then call egress from its main thread, in step (bench / tests)."""
         L = self.layout
-        if torch.cuda.current_stream(self.device) != self._ready_stream:
-            self._ready.synchronize()  # another stream wrote the model: the blocking copy alone would not wait
-        full = self.shards.all_gather(self._f[self._cur])
-        if L.P_full == f_cpu.numel():  # (a _HostBuf holds exactly P_full floats, at least one)
-            f_cpu.copy_(full[:L.P_full])
-        else:
-            f_cpu[:L.P_full].copy_(full[:L.P_full])
-        if L.Q:
-            s_cpu[:L.Q].copy_(self._s[self._cur][:L.Q])
+        es = self._egress_ds
+        if es is None:
+            es = self._egress_ds = DeviceStream(self.device)
+        with es:  # its own stream, ordered after the round's kernels by an event: one host wait, at the end
+            es.stream.wait_event(self._ready)
+            full = self.shards.all_gather(self._f[self._cur])
+            if L.P_full == f_cpu.numel():  # (a _HostBuf holds exactly P_full floats, at least one)
+                f_cpu.copy_(full[:L.P_full], non_blocking=True)
+            else:
+                f_cpu[:L.P_full].copy_(full[:L.P_full], non_blocking=True)
+            if L.Q:
+                s_cpu[:L.Q].copy_(self._s[self._cur][:L.Q], non_blocking=True)
+            es.stream.synchronize()
 
     def _acquire_host(self) -> "_HostSnapshot":
         """The host snapshot of the current model version (one D2H per version), held by the caller until
@@ -357,7 +362,7 @@ class TorchModelAdapter(ModelAdapterBase):
         """``keep_mean`` for q-FedAvg rounds: True fuses the FedAvg chain when the round spans several chunks
         (the staged updates are then gone by the end of the round), "always" in every round (the mean is then
         independent of the staging's later reuse), False never (model_weights of such rounds raises)."""
-        with self.dstream.joined():
+        with self.dstream:  # no join: nothing it queues (staging allocation) is read by the caller
             return self._begin_round(K, policy, capacity, keep_mean)
 
     def _begin_round(self, K, policy, capacity, keep_mean) -> DeviceRound:

@@ -747,12 +747,22 @@ __device__ __forceinline__ f4 rows_load(__amdgpu_buffer_rsrc_t r, uint32_t voff)
 // flight through the compute phase at no register cost (GLDS x 16 KiB of LDS per wave).  Measured
 // (profiles/r02_tune_qfed2.log): 2-4 % SLOWER than register loads for the plain kernel, 1-5 % FASTER with
 // the fused FedAvg chain (whose 64 extra live values otherwise go through AGPRs), so chain launches use it.
+// QF_CHAIN_LDS 1 (CHAIN launches with GLDS == 1): the FedAvg chain lives in LDS instead of registers — each
+// lane's own f4 slots (no barrier), updated from the landed row slice as it is copied to registers, so the 64
+// chain values no longer push the register design into AGPR parking.  LDS: 32 KiB sq + 64 KiB row slices +
+// 64 KiB chain = the whole 160 KiB of a gfx950 CU.
+#ifndef QF_CHAIN_LDS
+#define QF_CHAIN_LDS 0
+#endif
 template <bool WIDE, bool CHAIN, int GLDS>
 __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
   static_assert(GLDS == 0 || GLDS == 1 || (GLDS == 2 && QF_V == 16), "GLDS: 0, 1 or 2 LDS slices per wave");
   constexpr int NB = GLDS > 0 ? GLDS : 1;
+  constexpr bool CLDS = CHAIN && QF_CHAIN_LDS && GLDS == 1;
   __shared__ double sq[4][QF_MAXK];
   __shared__ f4 rowbuf[GLDS > 0 ? GLDS * 4 * QF_V * 64 : 1];  // GLDS 2: 128 KiB + 32 KiB sq = 160 KiB
+  __shared__ f4 chainbuf[CLDS ? 4 * QF_V * 64 : 1];
+  f4* const myc = chainbuf + (CLDS ? (threadIdx.x >> 6) * (QF_V * 64) + (threadIdx.x & 63) : 0);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < 4 * QF_MAXK; i += 256) (&sq[0][0])[i] = 0.0;
@@ -779,9 +789,14 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       L[j] = ok[j] ? reinterpret_cast<const f4*>(q.last)[c0 + 64 * j] : f4{0.f, 0.f, 0.f, 0.f};
       D[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.delta)[c0 + 64 * j]
                                                   : f4{0.f, 0.f, 0.f, 0.f};
-      if (CHAIN)
-        C[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.chain)[c0 + 64 * j]
-                                                    : f4{0.f, 0.f, 0.f, 0.f};
+      if (CHAIN) {
+        const f4 c = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.chain)[c0 + 64 * j]
+                                                          : f4{0.f, 0.f, 0.f, 0.f};
+        if (CLDS)
+          myc[64 * j] = c;
+        else
+          C[j] = c;
+      }
     }
     // one client: g = (L - W)/lr from its loaded row slice t (overwritten with L - W), delta chain and the
     // lane's fp64 sum of squares
@@ -791,7 +806,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       DivRange rng;
 #pragma unroll
       for (int j = 0; j < QF_V; ++j) {
-        if (CHAIN) C[j] = first ? t[j] : C[j] + t[j];  // the FedAvg chain of the same upload
+        if (CHAIN && !CLDS) C[j] = first ? t[j] : C[j] + t[j];  // the FedAvg chain of the same upload
         t[j] = L[j] - t[j];  // (last - W), optimizers.py:83; the "* 1.0" is exact
         g[j].x = fast_div(t[j].x, q.lr, q.rlr);
         g[j].y = fast_div(t[j].y, q.lr, q.rlr);
@@ -890,6 +905,11 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
         const f4* src = myrow + (kk % NB) * (QF_V * 64);
 #pragma unroll
         for (int j = 0; j < QF_V; ++j) t[j] = src[64 * j];
+        if constexpr (CLDS) {  // the FedAvg chain of the same upload, in LDS (aggregator.py:500-503)
+          const bool first = (kk == 0) && !(q.flags & FA_ACCUMULATE);
+#pragma unroll
+          for (int j = 0; j < QF_V; ++j) myc[64 * j] = first ? t[j] : myc[64 * j] + t[j];
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and is in registers: refill the slot
         const float al = al_q[0];
 #pragma unroll
@@ -973,7 +993,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
     for (int j = 0; j < QF_V; ++j)
       if (ok[j]) {
         reinterpret_cast<f4*>(q.delta)[c0 + 64 * j] = D[j];
-        if (CHAIN) reinterpret_cast<f4*>(q.chain)[c0 + 64 * j] = C[j];
+        if (CHAIN) reinterpret_cast<f4*>(q.chain)[c0 + 64 * j] = CLDS ? myc[64 * j] : C[j];
       }
   }
   __syncthreads();

@@ -43,7 +43,7 @@ class DeviceStream:
     current device).  Work the adapter does not own — device tensors handed in by the caller — is ordered
     by ``wait_caller()``: the stream waits for the stream that was current on this device at entry."""
 
-    __slots__ = ("device", "index", "stream", "handle")
+    __slots__ = ("device", "index", "stream", "handle", "_join_ev")
     _tls = threading.local()
 
     def __init__(self, device, stream: "Optional[torch.cuda.Stream]" = None):
@@ -55,6 +55,7 @@ class DeviceStream:
         self.device, self.index = d, d.index
         self.stream = stream if stream is not None else torch.cuda.Stream(device=d)
         self.handle = self.stream.cuda_stream  # never 0: a stream of this device, not the null stream
+        self._join_ev = None  # one event, re-recorded for every join (no event create/destroy per call)
 
     @classmethod
     def current(cls) -> "Optional[DeviceStream]":
@@ -79,8 +80,12 @@ class DeviceStream:
 
     def _exit(self, join: bool):
         _, prev_dev, prev = self._tls.stack.pop()
-        if join and prev != self.stream:
-            prev.wait_stream(self.stream)  # no host sync: the caller's stream is ordered after our work
+        if join and prev != self.stream:  # no host sync: the caller's stream is ordered after our work
+            ev = self._join_ev
+            if ev is None:
+                ev = self._join_ev = torch.cuda.Event()
+            ev.record(self.stream)
+            prev.wait_event(ev)
         torch.cuda.set_stream(prev)
         if prev_dev != self.index:
             torch.cuda.set_device(prev_dev)

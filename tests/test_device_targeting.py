@@ -30,6 +30,17 @@ class FakeStream:
     def wait_stream(self, other):
         self.waited.append(other)
 
+    def wait_event(self, ev):
+        self.waited.append(ev.src)
+
+
+class FakeEvent:
+    def __init__(self, *a, **k):
+        self.src = None
+
+    def record(self, stream=None):
+        self.src = stream
+
 
 class FakeCuda:
     """torch.cuda as seen by one thread: a current device and a current stream per device."""
@@ -44,6 +55,7 @@ class FakeCuda:
         monkeypatch.setattr(torch.cuda, "current_stream", self.current_stream)
         monkeypatch.setattr(torch.cuda, "set_stream", self.set_stream)
         monkeypatch.setattr(torch.cuda, "Stream", self.new_stream)
+        monkeypatch.setattr(torch.cuda, "Event", FakeEvent)
 
     def set_device(self, d):
         assert 0 <= int(d) < self.ndev
