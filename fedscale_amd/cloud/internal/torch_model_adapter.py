@@ -362,10 +362,6 @@ class TorchModelAdapter(ModelAdapterBase):
         """``keep_mean`` for q-FedAvg rounds: True fuses the FedAvg chain when the round spans several chunks
         (the staged updates are then gone by the end of the round), "always" in every round (the mean is then
         independent of the staging's later reuse), False never (model_weights of such rounds raises)."""
-        with self.dstream:  # no join: nothing it queues (staging allocation) is read by the caller
-            return self._begin_round(K, policy, capacity, keep_mean)
-
-    def _begin_round(self, K, policy, capacity, keep_mean) -> DeviceRound:
         cap = capacity or self.staging_capacity
         K_local = K
         if self.shards.shards_clients:  # this rank stages only its block of the arrivals

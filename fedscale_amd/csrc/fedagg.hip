@@ -142,6 +142,9 @@ struct RedArgs {
 #ifndef FA_RED_WAVES
 #define FA_RED_WAVES 4
 #endif
+#ifndef FA_PIPE
+#define FA_PIPE 0  // 1: software-pipelined client groups in reduce_tile (tuning option)
+#endif
 // One tile: the workgroup's FA_RED_WAVES waves each own 64*sw float4 columns (sw <= V strips, a run-time
 // width; FULL: sw == V, the compile-time width) and walk all K clients.
 template <int V, int U, int EPI, bool W, bool FULL>
@@ -171,19 +174,45 @@ __device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int 
   }
 
   const f4* row = xp + (int64_t)k * r.ld4 + c0;
-  for (; k + U <= r.K; k += U) {
-    f4 t[U][V];
+  // U clients' loads, then their adds in arrival order
+  auto load_group = [&](f4(&t)[U][V], const f4* rw) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < V; ++j)
-        t[u][j] = ok[j] ? ldnt(row + u * r.ld4 + 64 * j) : f4{0.f, 0.f, 0.f, 0.f};
+        t[u][j] = ok[j] ? ldnt(rw + u * r.ld4 + 64 * j) : f4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto add_group = [&](const f4(&t)[U][V], int k0) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float w = W ? r.a[k + u] : 1.f;
+      const float w = W ? r.a[k0 + u] : 1.f;
 #pragma unroll
       for (int j = 0; j < V; ++j) s[j] = W ? s[j] + w * t[u][j] : s[j] + t[u][j];
     }
+  };
+  if (FA_PIPE && k + U <= r.K) {
+    // software pipeline: the next group's loads are issued before the current group's adds, so every wave
+    // keeps U*V KiB in flight through its add phase too (two register buffers, alternating)
+    f4 ta[U][V], tb[U][V];
+    load_group(ta, row);
+    row += U * r.ld4;
+    for (;;) {
+      const bool more = k + 2 * U <= r.K;
+      if (more) load_group(tb, row), row += U * r.ld4;
+      add_group(ta, k);
+      k += U;
+      if (!more) break;
+      const bool more2 = k + 2 * U <= r.K;
+      if (more2) load_group(ta, row), row += U * r.ld4;
+      add_group(tb, k);
+      k += U;
+      if (!more2) break;
+    }
+  }
+  for (; k + U <= r.K; k += U) {
+    f4 t[U][V];
+    load_group(t, row);
+    add_group(t, k);
     row += U * r.ld4;
   }
   for (; k < r.K; ++k) {

@@ -11,6 +11,7 @@ import torch
 
 from . import _native as N
 from ._native import FA_ACCUMULATE, FA_FINALIZE, FA_YOGI_INIT, call, ptr
+from .state import raw_stream
 
 
 def _dev(t: torch.Tensor, dtype, name: str, min_numel: int = 0, align: int = 16):
@@ -33,7 +34,8 @@ def _cols(P: int) -> int:
 
 
 def _stream(t: torch.Tensor):
-    return torch.cuda.current_stream(t.device).cuda_stream
+    """The current stream of the tensor's device on this thread (an adapter's DeviceStream inside its calls)."""
+    return raw_stream(t.device.index)
 
 
 def _check_x(x: torch.Tensor, K: int, P: int):

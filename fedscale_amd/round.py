@@ -23,6 +23,7 @@ import torch
 
 from . import kernels as kx
 from .bucket import BucketLayout, ClientStaging
+from .bucket import _NULL_CTX as _NULL
 from .state import DeviceStream, ShardGroup
 
 POLICIES = ("fedavg", "fedbuff", "qfedavg")
@@ -68,8 +69,14 @@ class DeviceRound:
         self.dstream = dstream
         self._init(layout, device, K, policy, capacity, staging, last_f32, last_i64, clients, mean_chain)
 
-    @on_stream
+    def _on(self):
+        """Context for GPU work of this round: its dstream unless already current (or none)."""
+        ds = self.dstream
+        return _NULL if ds is None or DeviceStream.current() is ds else ds
+
     def _init(self, layout, device, K, policy, capacity, staging, last_f32, last_i64, clients, mean_chain):
+        """(steady-state FedAvg / FedBuff rounds reuse the staging and its side-table scratch: no GPU work,
+        so no device context is entered; allocations are made on the dstream)"""
         if policy not in POLICIES:
             raise ValueError(f"policy {policy!r} not in {POLICIES}")
         if K < 1:
@@ -103,30 +110,38 @@ class DeviceRound:
         if self.cg is None and policy in ("fedavg", "fedbuff"):
             # consumed by finalize_mean before the next round can begin: one pair per staging, reused
             if self.staging.side_scratch is None:
-                self.staging.side_scratch = (torch.empty(L.ldq, dtype=torch.int64, device=dev),
-                                             torch.empty(L.ldq, dtype=torch.float64, device=dev))
+                with self._on():
+                    self.staging.side_scratch = (torch.empty(L.ldq, dtype=torch.int64, device=dev),
+                                                 torch.empty(L.ldq, dtype=torch.float64, device=dev))
             self.acc_i, self.acc_d = self.staging.side_scratch
         else:  # q-FedAvg keeps them for the round's lazily computed mean (mean_from_staging)
             alloc = torch.zeros if self.cg is not None else torch.empty
-            self.acc_i = alloc(L.ldq, dtype=torch.int64, device=dev)
-            self.acc_d = alloc(L.ldq, dtype=torch.float64, device=dev)
+            with self._on():
+                self.acc_i = alloc(L.ldq, dtype=torch.int64, device=dev)
+                self.acc_d = alloc(L.ldq, dtype=torch.float64, device=dev)
         self._w32 = np.zeros(self.cap, dtype=np.float32)  # per-slot weights of the current chunk
         self._w64 = np.zeros(self.cap, dtype=np.float64)
         self.last_f32, self.last_i64 = last_f32, last_i64
         if policy == "qfedavg":
             if last_f32 is None or last_i64 is None:
                 raise ValueError("q-FedAvg needs the round's starting model (last_f32 / last_i64)")
-            self.delta = torch.zeros(L.ld, dtype=torch.float32, device=dev)
-            self.delta_s = torch.zeros(L.ldq, dtype=torch.float32, device=dev)
-            self.sqnorm = torch.zeros(self.K, dtype=torch.float64, device=dev)       # fp32 bucket part (per shard)
-            self.sqnorm_side = torch.zeros(self.K, dtype=torch.float64, device=dev)  # side table part (replicated)
-            self.workspace = kx.qfed_workspace(self.cap, dev)
-            self.alpha = np.zeros(self.K, dtype=np.float32)
-            self.c1 = np.zeros(self.K, dtype=np.float32)
-            self.c2 = np.zeros(self.K, dtype=np.float32)
-            self.lr = None
-        self.chain = (torch.zeros(L.ld, dtype=torch.float32, device=dev)
-                      if policy == "qfedavg" and mean_chain and self.cg is None else None)
+            with self._on():
+                self._init_qfed(L, dev)
+        self.chain = None
+        if policy == "qfedavg" and mean_chain and self.cg is None:
+            with self._on():
+                self.chain = torch.zeros(L.ld, dtype=torch.float32, device=dev)
+
+    def _init_qfed(self, L, dev):
+        self.delta = torch.zeros(L.ld, dtype=torch.float32, device=dev)
+        self.delta_s = torch.zeros(L.ldq, dtype=torch.float32, device=dev)
+        self.sqnorm = torch.zeros(self.K, dtype=torch.float64, device=dev)       # fp32 bucket part (per shard)
+        self.sqnorm_side = torch.zeros(self.K, dtype=torch.float64, device=dev)  # side table part (replicated)
+        self.workspace = kx.qfed_workspace(self.cap, dev)
+        self.alpha = np.zeros(self.K, dtype=np.float32)
+        self.c1 = np.zeros(self.K, dtype=np.float32)
+        self.c2 = np.zeros(self.K, dtype=np.float32)
+        self.lr = None
 
     # ---------------------------------------------------------------------------------------------
     def add(self, update, *, weight: Optional[float] = None, loss: Optional[float] = None,

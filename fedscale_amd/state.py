@@ -24,13 +24,67 @@ from __future__ import annotations
 
 import atexit
 import threading
-import weakref
 from dataclasses import dataclass
 from typing import Optional
 
 import torch
 
 from .bucket import BucketLayout
+
+
+# Thin wrappers over torch's per-thread device / current-stream state.  A stream is named by its key
+# (stream_id, device_index, device_type); the raw torch._C calls skip torch.cuda.current_stream()'s Stream-object
+# construction, which costs several µs per call on the per-round path (config 1 rounds take ~0.1 ms).
+_C = torch._C
+_FAST = all(hasattr(_C, n) for n in ("_cuda_getDevice", "_cuda_setDevice", "_cuda_getCurrentStream",
+                                      "_cuda_setStream", "_cuda_getCurrentRawStream"))
+
+
+def _get_device() -> int:
+    return _C._cuda_getDevice() if _FAST else torch.cuda.current_device()
+
+
+def _set_device(i: int):
+    if _FAST:
+        _C._cuda_setDevice(i)
+    else:
+        torch.cuda.set_device(i)
+
+
+def _stream_key(s) -> tuple:
+    return (s.stream_id, s.device_index, s.device_type)
+
+
+def _get_stream(i: int) -> tuple:
+    """Key of the current stream of device i (this thread)."""
+    if _FAST:
+        return tuple(_C._cuda_getCurrentStream(i))
+    return _stream_key(torch.cuda.current_stream(i))
+
+
+def _set_stream(key: tuple):
+    if _FAST:
+        _C._cuda_setStream(stream_id=key[0], device_index=key[1], device_type=key[2])
+    else:
+        torch.cuda.set_stream(_stream_obj(key))
+
+
+_STREAM_OBJS: dict = {}
+
+
+def _stream_obj(key: tuple):
+    """A torch Stream object for a key (cached: callers' streams are few, usually the default one)."""
+    s = _STREAM_OBJS.get(key)
+    if s is None:
+        s = _STREAM_OBJS[key] = torch.cuda.Stream(stream_id=key[0], device_index=key[1], device_type=key[2])
+    return s
+
+
+def raw_stream(index: int) -> int:
+    """hipStream_t of the current stream of device ``index`` on this thread (what the C ABI takes)."""
+    if _FAST:
+        return _C._cuda_getCurrentRawStream(index)
+    return torch.cuda.current_stream(index).cuda_stream
 
 
 class DeviceStream:
@@ -43,7 +97,7 @@ class DeviceStream:
     current device).  Work the adapter does not own — device tensors handed in by the caller — is ordered
     by ``wait_caller()``: the stream waits for the stream that was current on this device at entry."""
 
-    __slots__ = ("device", "index", "stream", "handle", "_join_ev")
+    __slots__ = ("device", "index", "stream", "handle", "key", "_join_ev")
     _tls = threading.local()
 
     def __init__(self, device, stream: "Optional[torch.cuda.Stream]" = None):
@@ -51,10 +105,11 @@ class DeviceStream:
         if d.type != "cuda":
             raise ValueError(f"device {d}: the aggregation path runs on the GPU only (no CPU fallback)")
         if d.index is None:
-            d = torch.device("cuda", torch.cuda.current_device())
+            d = torch.device("cuda", _get_device())
         self.device, self.index = d, d.index
         self.stream = stream if stream is not None else torch.cuda.Stream(device=d)
         self.handle = self.stream.cuda_stream  # never 0: a stream of this device, not the null stream
+        self.key = _stream_key(self.stream)
         self._join_ev = None  # one event, re-recorded for every join (no event create/destroy per call)
 
     @classmethod
@@ -67,11 +122,11 @@ class DeviceStream:
         st = getattr(self._tls, "stack", None)
         if st is None:
             st = self._tls.stack = []
-        prev_dev = torch.cuda.current_device()
+        prev_dev = _get_device()
         if prev_dev != self.index:
-            torch.cuda.set_device(self.index)
-        prev = torch.cuda.current_stream(self.index)  # the caller's stream on this device
-        torch.cuda.set_stream(self.stream)
+            _set_device(self.index)
+        prev = _get_stream(self.index)  # the caller's stream on this device
+        _set_stream(self.key)
         st.append((self, prev_dev, prev))
         return self
 
@@ -80,15 +135,15 @@ class DeviceStream:
 
     def _exit(self, join: bool):
         _, prev_dev, prev = self._tls.stack.pop()
-        if join and prev != self.stream:  # no host sync: the caller's stream is ordered after our work
+        if join and prev != self.key:  # no host sync: the caller's stream is ordered after our work
             ev = self._join_ev
             if ev is None:
                 ev = self._join_ev = torch.cuda.Event()
             ev.record(self.stream)
-            prev.wait_event(ev)
-        torch.cuda.set_stream(prev)
+            _stream_obj(prev).wait_event(ev)
+        _set_stream(prev)
         if prev_dev != self.index:
-            torch.cuda.set_device(prev_dev)
+            _set_device(prev_dev)
         return False
 
     def joined(self) -> "_Joined":
@@ -102,12 +157,12 @@ class DeviceStream:
         """Order this stream after the work the caller queued on this device before its outermost entry."""
         for ds, _, prev in getattr(self._tls, "stack", None) or ():
             if ds is self:
-                if prev != self.stream:
-                    self.stream.wait_stream(prev)
+                if prev != self.key:
+                    self.stream.wait_stream(_stream_obj(prev))
                 return
-        cur = torch.cuda.current_stream(self.index)
-        if cur != self.stream:
-            self.stream.wait_stream(cur)
+        cur = _get_stream(self.index)
+        if cur != self.key:
+            self.stream.wait_stream(_stream_obj(cur))
 
 
 class _Joined:

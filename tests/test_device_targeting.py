@@ -24,7 +24,9 @@ class FakeStream:
     def __init__(self, dev: int, handle=None):
         self.device_index = dev
         self.device = torch.device("cuda", dev)
+        self.device_type = 1
         self.cuda_stream = next(self._ids) if handle is None else handle
+        self.stream_id = self.cuda_stream
         self.waited = []
 
     def wait_stream(self, other):
@@ -43,17 +45,23 @@ class FakeEvent:
 
 
 class FakeCuda:
-    """torch.cuda as seen by one thread: a current device and a current stream per device."""
+    """torch.cuda as seen by one thread: a current device and a current stream per device (the state.py
+    helpers that read and set them are replaced)."""
 
     def __init__(self, monkeypatch, ndev: int, current: int = 0):
+        from fedscale_amd import state
+
         self.cur = current
         self.ndev = ndev
         self.default = {d: FakeStream(d, 0) for d in range(ndev)}  # torch's default stream: handle 0
         self.stream_of = dict(self.default)
-        monkeypatch.setattr(torch.cuda, "current_device", lambda: self.cur)
-        monkeypatch.setattr(torch.cuda, "set_device", self.set_device)
+        self.by_key = {state._stream_key(s): s for s in self.default.values()}
+        monkeypatch.setattr(state, "_get_device", lambda: self.cur)
+        monkeypatch.setattr(state, "_set_device", self.set_device)
+        monkeypatch.setattr(state, "_get_stream", lambda i: state._stream_key(self.stream_of[i]))
+        monkeypatch.setattr(state, "_set_stream", lambda key: self.set_stream(self.by_key[key]))
+        monkeypatch.setattr(state, "_stream_obj", lambda key: self.by_key[key])
         monkeypatch.setattr(torch.cuda, "current_stream", self.current_stream)
-        monkeypatch.setattr(torch.cuda, "set_stream", self.set_stream)
         monkeypatch.setattr(torch.cuda, "Stream", self.new_stream)
         monkeypatch.setattr(torch.cuda, "Event", FakeEvent)
 
@@ -68,7 +76,17 @@ class FakeCuda:
         self.stream_of[s.device_index] = s
 
     def new_stream(self, device=None):
-        return FakeStream(torch.device(device).index)
+        from fedscale_amd import state
+
+        s = FakeStream(torch.device(device).index)
+        self.by_key[state._stream_key(s)] = s
+        return s
+
+    def adopt(self, s):
+        from fedscale_amd import state
+
+        self.by_key[state._stream_key(s)] = s
+        return s
 
 
 def test_device_stream_targets_its_device_whatever_is_current(monkeypatch):
@@ -98,7 +116,7 @@ def test_device_stream_joined_and_wait_caller(monkeypatch):
     from fedscale_amd.state import DeviceStream
 
     fc = FakeCuda(monkeypatch, 2, current=1)
-    caller = FakeStream(0)
+    caller = fc.adopt(FakeStream(0))
     fc.stream_of[0] = caller  # the caller works on its own stream of device 0
     ds = DeviceStream(0)
     with ds.joined():
