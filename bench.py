@@ -82,6 +82,9 @@ def parse():
     ap.add_argument("--mem-fraction", type=float, default=0.6,
                     help="share of the free HBM a workload's resident client chunk may take (lower it when several "
                          "ranks share one GPU in a rehearsal)")
+    ap.add_argument("--sets", type=int, default=None,
+                    help="rotating resident input sets (default 1; 2 for --config c2, whose 400 MB would otherwise "
+                         "be served partly by the 256 MiB Infinity Cache)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo only to rehearse ranks sharing a GPU")
     a = ap.parse_args()
@@ -615,7 +618,9 @@ def main():
     weak = args.scaling == "weak"
     global MEM_FRACTION
     MEM_FRACTION = args.mem_fraction
-    w = Workload(policy, K, P, rank, world, dev, args.seed, shards, weak=weak, budget_fraction=args.mem_fraction)
+    sets = args.sets if args.sets is not None else (2 if args.config == "c2" else 1)
+    w = Workload(policy, K, P, rank, world, dev, args.seed, shards, weak=weak, budget_fraction=args.mem_fraction,
+                 sets=sets)
     (wall, kern_ms_max), kern_ms, kern_ms_ranks = time_workload(w, args.steps, args.warmup, dev, world,
                                                                  args.dist_backend)
     pg_world = dist.get_world_size() if world > 1 else 1
@@ -632,12 +637,13 @@ def main():
         reassembly_ms = _max_over_ranks([(time.perf_counter() - t0r) * 1e3 / 5], dev, world, args.dist_backend)[0]
     alg_bytes = w.alg_bytes
     P_local, n_passes = w.P, len(w.passes)
+    w_chain = bool(getattr(w, "qf", None) and w.qf.get("chain") is not None)
     w_ld = w.ld
     # launches of the dominant kernel per step: fa_reduce runs long buckets as column windows (fedagg.hip
     # FA_WINDOWS), so the per-launch figures rocprof reports are the step's divided by this
     from fedscale_amd import kernels as kx
     if policy == "qfedavg":
-        launches = n_passes * kx.qfed_launches(w_ld, P_local)
+        launches = n_passes * kx.qfed_launches(w_ld, P_local, chain=w_chain)
     else:
         launches = n_passes * kx.reduce_launches(w.C if n_passes > 1 else K, P_local, weighted=policy == "fedbuff")
     w.free()

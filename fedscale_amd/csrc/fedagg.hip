@@ -143,11 +143,11 @@ struct RedArgs {
 #define FA_RED_WAVES 4
 #endif
 #ifndef FA_PIPE
-#define FA_PIPE 0  // 1: software-pipelined client groups in reduce_tile (tuning option)
+#define FA_PIPE 0  // 1: every variant software-pipelines its client groups (tuning builds)
 #endif
 // One tile: the workgroup's FA_RED_WAVES waves each own 64*sw float4 columns (sw <= V strips, a run-time
 // width; FULL: sw == V, the compile-time width) and walk all K clients.
-template <int V, int U, int EPI, bool W, bool FULL>
+template <int V, int U, int EPI, bool W, bool FULL, bool PIPE = false>
 __device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int lane, int wave) {
   const f4* __restrict__ xp = reinterpret_cast<const f4*>(r.x);
   const int sw = FULL ? V : r.sw;
@@ -190,7 +190,7 @@ __device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int 
       for (int j = 0; j < V; ++j) s[j] = W ? s[j] + w * t[u][j] : s[j] + t[u][j];
     }
   };
-  if (FA_PIPE && k + U <= r.K) {
+  if ((PIPE || FA_PIPE) && k + U <= r.K) {
     // software pipeline: the next group's loads are issued before the current group's adds, so every wave
     // keeps U*V KiB in flight through its add phase too (two register buffers, alternating)
     f4 ta[U][V], tb[U][V];
@@ -262,7 +262,7 @@ __device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int 
 // LOOP = false: workgroup b reduces tile b (grid = tiles).  LOOP = true: a capped grid, workgroup b
 // reduces tiles b, b + grid, ... (r.ntiles in this launch): fewer concurrent column streams per round.
 // FULL: the tiles are V strips wide (r.sw == V, compile-time masks); otherwise r.sw < V at run time.
-template <int V, int U, int EPI, bool W, bool LOOP, bool FULL = true>
+template <int V, int U, int EPI, bool W, bool LOOP, bool FULL = true, bool PIPE = false>
 __global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -276,9 +276,9 @@ __global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
       b = x * q + (x < rem ? x : rem) + b / 8;
     }
 #endif
-    for (int64_t tile = b; tile < r.ntiles; tile += gridDim.x) reduce_tile<V, U, EPI, W, FULL>(r, tile, lane, wave);
+    for (int64_t tile = b; tile < r.ntiles; tile += gridDim.x) reduce_tile<V, U, EPI, W, FULL, PIPE>(r, tile, lane, wave);
   } else {
-    reduce_tile<V, U, EPI, W, FULL>(r, blockIdx.x, lane, wave);
+    reduce_tile<V, U, EPI, W, FULL, PIPE>(r, blockIdx.x, lane, wave);
   }
 }
 
@@ -461,6 +461,23 @@ static void launch_window(RedArgs r, int64_t s0, int64_t ns, int64_t cap, hipStr
 #ifndef FA_WINDOWS
 #define FA_WINDOWS 1
 #endif
+// Short, narrow rounds (config 2: 100 x 1 M, 400 MB per round): one launch, one workgroup per tile of 4
+// waves x 4 float4 per lane, the client groups software-pipelined (two register buffers of 4 clients: the
+// next group's 16 KiB per wave is in flight while the current one is added, so 32 KiB per wave is
+// outstanding through the add phase).  Round 2 ran a cascade of up to 4 launches of narrower variants here.
+// Measured against a bare stream read of the same 400 MB in the same process (tools/c2_probe.py,
+// profiles/r03_c2_probe.log): the cascade 97.4 %, this launch 98.3 %.
+#ifndef FA_SHORT_PIPE
+#define FA_SHORT_PIPE 1
+#endif
+template <int EPI, bool W>
+static void launch_short(RedArgs r, hipStream_t st) {
+  const int64_t span = 64LL * FA_RED_WAVES * 4;
+  r.col0 = 0;
+  r.sw = 4;
+  r.ntiles = (r.P4 + span - 1) / span;
+  FA_RED_LAUNCH((k_reduce<4, 4, EPI, W, false, true, true>), dim3((unsigned)r.ntiles), dim3(64 * FA_RED_WAVES), st, r);
+}
 template <int EPI, bool W>
 static void launch_plan(const RedArgs& r, hipStream_t st) {
   int64_t col = 0;
@@ -511,6 +528,12 @@ static void launch_plan(const RedArgs& r, hipStream_t st) {
         launch_balanced<8, 4, EPI, W>(r, swb, 1, st);
       return;
     }
+  }
+#endif
+#if FA_SHORT_PIPE
+  if (cap > 0) {  // narrow, short round (K x sw < FA_BAL_MIN_WORK, e.g. config 2's 100 x 1 M)
+    launch_short<EPI, W>(r, st);
+    return;
   }
 #endif
   if (cap > 0 && tiles0 * 20 >= cap * 17) {  // enough widest tiles to keep ~cap workgroups busy
@@ -765,6 +788,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rows_rsrc(const float* row0, u
 __device__ __forceinline__ f4 rows_load(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
   return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, 2));
 }
+// 16 B per lane HBM -> LDS (buffer_load_dwordx4 ... lds, non-temporal): lane i's bytes land at LDS address
+// lds + 16 i.  A plain device function, so the kernel templates that call it stay valid in the host pass.
+__device__ __forceinline__ void rows_load_lds(__amdgpu_buffer_rsrc_t r, uint32_t lds, uint32_t voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(uintptr_t)lds, 16, voff, 0,
+                                           0, 2);
+}
 
 #ifndef QF_MINW
 #define QF_MINW 1
@@ -776,29 +805,23 @@ __device__ __forceinline__ f4 rows_load(__amdgpu_buffer_rsrc_t r, uint32_t voff)
 // flight through the compute phase at no register cost (GLDS x 16 KiB of LDS per wave).  Measured
 // (profiles/r02_tune_qfed2.log): 2-4 % SLOWER than register loads for the plain kernel, 1-5 % FASTER with
 // the fused FedAvg chain (whose 64 extra live values otherwise go through AGPRs), so chain launches use it.
-// QF_CHAIN_LDS 1 (CHAIN launches with GLDS == 1): the FedAvg chain lives in LDS instead of registers — each
-// lane's own f4 slots (no barrier), updated from the landed row slice as it is copied to registers, so the 64
-// chain values no longer push the register design into AGPR parking.  LDS: 32 KiB sq + 64 KiB row slices +
-// 64 KiB chain = the whole 160 KiB of a gfx950 CU.
-#ifndef QF_CHAIN_LDS
-#define QF_CHAIN_LDS 0
-#endif
-template <bool WIDE, bool CHAIN, int GLDS>
+template <bool WIDE, bool CHAIN, int GLDS, int QV>
 __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
-  static_assert(GLDS == 0 || GLDS == 1 || (GLDS == 2 && QF_V == 16), "GLDS: 0, 1 or 2 LDS slices per wave");
+  static_assert(GLDS == 0 || GLDS == 1 || (GLDS == 2 && QV == 16), "GLDS: 0, 1 or 2 LDS slices per wave");
   constexpr int NB = GLDS > 0 ? GLDS : 1;
-  constexpr bool CLDS = CHAIN && QF_CHAIN_LDS && GLDS == 1;
-  __shared__ double sq[4][QF_MAXK];
-  __shared__ f4 rowbuf[GLDS > 0 ? GLDS * 4 * QF_V * 64 : 1];  // GLDS 2: 128 KiB + 32 KiB sq = 160 KiB
-  __shared__ f4 chainbuf[CLDS ? 4 * QF_V * 64 : 1];
-  f4* const myc = chainbuf + (CLDS ? (threadIdx.x >> 6) * (QF_V * 64) + (threadIdx.x & 63) : 0);
+  // ONE static LDS array, so it sits at LDS offset 0: the row slices first (the DMA addresses them from
+  // offset 0), then the per-client squared norms sq[4][QF_MAXK].  GLDS 2: 128 KiB + 32 KiB = 160 KiB.
+  constexpr int ROWB = GLDS > 0 ? GLDS * 4 * QV * 64 : 0;  // f4 elements of row slices
+  __shared__ f4 lds_all[ROWB + 4 * QF_MAXK / 2];
+  f4* const rowbuf = lds_all;
+  double(*const sq)[QF_MAXK] = reinterpret_cast<double(*)[QF_MAXK]>(lds_all + ROWB);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   for (int i = threadIdx.x; i < 4 * QF_MAXK; i += 256) (&sq[0][0])[i] = 0.0;
   __syncthreads();
 
   // Balanced grid-stride: the columns come in strips of 64 f4 (one wave-wide dwordx4 load).  A tile is
-  // 4 waves x sw strips, sw <= QF_V chosen so that the tiles divide evenly over the grid (fa_qfed_
+  // 4 waves x sw strips, sw <= QV chosen so that the tiles divide evenly over the grid (fa_qfed_
   // accumulate: q.sw) — no workgroup is left with an extra tile whatever P is — and the workgroups
   // stride over tiles so the grid's concurrent loads stay on adjacent addresses.
   const int64_t S = (q.P4 + 63) / 64;
@@ -808,34 +831,29 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
   for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int64_t sw0 = tile * 4 * sw + (int64_t)wave * sw;  // this wave's first strip
     const int64_t c0 = sw0 * 64 + lane;
-    bool ok[QF_V];
-    f4 L[QF_V], D[QF_V], C[QF_V];
-    uint32_t voff[QF_V];  // byte offset of this lane's column j in a row, or QF_OOB
+    bool ok[QV];
+    f4 L[QV], D[QV], C[QV];
+    uint32_t voff[QV];  // byte offset of this lane's column j in a row, or QF_OOB
 #pragma unroll
-    for (int j = 0; j < QF_V; ++j) {
+    for (int j = 0; j < QV; ++j) {
       ok[j] = j < sw && (c0 + 64 * j) < q.P4;
       voff[j] = ok[j] ? (uint32_t)((c0 + 64 * j) * 16) : QF_OOB;
       L[j] = ok[j] ? reinterpret_cast<const f4*>(q.last)[c0 + 64 * j] : f4{0.f, 0.f, 0.f, 0.f};
       D[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.delta)[c0 + 64 * j]
                                                   : f4{0.f, 0.f, 0.f, 0.f};
-      if (CHAIN) {
-        const f4 c = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.chain)[c0 + 64 * j]
-                                                          : f4{0.f, 0.f, 0.f, 0.f};
-        if (CLDS)
-          myc[64 * j] = c;
-        else
-          C[j] = c;
-      }
+      if (CHAIN)
+        C[j] = (ok[j] && (q.flags & FA_ACCUMULATE)) ? reinterpret_cast<const f4*>(q.chain)[c0 + 64 * j]
+                                                    : f4{0.f, 0.f, 0.f, 0.f};
     }
     // one client: g = (L - W)/lr from its loaded row slice t (overwritten with L - W), delta chain and the
     // lane's fp64 sum of squares
-    auto client = [&](f4(&t)[QF_V], int kk, float al) -> double {
+    auto client = [&](f4(&t)[QV], int kk, float al) -> double {
       const bool first = (kk == 0) && !(q.flags & FA_ACCUMULATE);
-      f4 g[QF_V];
+      f4 g[QV];
       DivRange rng;
 #pragma unroll
-      for (int j = 0; j < QF_V; ++j) {
-        if (CHAIN && !CLDS) C[j] = first ? t[j] : C[j] + t[j];  // the FedAvg chain of the same upload
+      for (int j = 0; j < QV; ++j) {
+        if (CHAIN) C[j] = first ? t[j] : C[j] + t[j];  // the FedAvg chain of the same upload
         t[j] = L[j] - t[j];  // (last - W), optimizers.py:83; the "* 1.0" is exact
         g[j].x = fast_div(t[j].x, q.lr, q.rlr);
         g[j].y = fast_div(t[j].y, q.lr, q.rlr);
@@ -848,7 +866,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       }
       double acc = 0.0;
 #pragma unroll
-      for (int j = 0; j < QF_V; j += QF_PART / 4) {
+      for (int j = 0; j < QV; j += QF_PART / 4) {
         float s = 0.f;
 #pragma unroll
         for (int i = 0; i < QF_PART / 4; ++i) {
@@ -866,14 +884,14 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       if (!q.fast || !__all(fast_ok)) {  // rare: redo this client with the IEEE division
         acc = 0.0;
 #pragma unroll
-        for (int j = 0; j < QF_V; ++j) {
+        for (int j = 0; j < QV; ++j) {
           g[j].x = __fdiv_rn(t[j].x, q.lr);
           g[j].y = __fdiv_rn(t[j].y, q.lr);
           g[j].z = __fdiv_rn(t[j].z, q.lr);
           g[j].w = __fdiv_rn(t[j].w, q.lr);
         }
 #pragma unroll
-        for (int j = 0; j < QF_V; j += QF_PART / 4) {  // the same partials as the fast path
+        for (int j = 0; j < QV; j += QF_PART / 4) {  // the same partials as the fast path
           float s = 0.f;
 #pragma unroll
           for (int i = 0; i < QF_PART / 4; ++i) {
@@ -885,26 +903,25 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
         }
       }
 #pragma unroll
-      for (int j = 0; j < QF_V; ++j) {
+      for (int j = 0; j < QV; ++j) {
         const f4 term = al * g[j];  // optimizers.py:89,93  float_power(...) * grad (fp32 product)
         D[j] = first ? term : D[j] + term;
       }
       return acc;
     };
-    f4* myrow = rowbuf + (GLDS > 0 ? wave * (NB * QF_V * 64) + lane : 0);
-    const uint32_t ldsbase = (uint32_t)__builtin_amdgcn_readfirstlane(wave) * (NB * QF_V * 64 * 16);
+    f4* myrow = rowbuf + (GLDS > 0 ? wave * (NB * QV * 64) + lane : 0);
+    // the DMA takes an absolute LDS address: rowbuf is at offset 0 of the kernel's only LDS array (with two
+    // LDS variables the compiler may place either first — round 2's layout worked by that accident)
+    const uint32_t ldsbase = (uint32_t)__builtin_amdgcn_readfirstlane(wave) * (NB * QV * 64 * 16);
     // client k's row slice -> this wave's LDS buffer (OOB lanes write 0).  Issued for every client,
     // k == K included (an empty range: zeros, no memory access), so the wait counts stay the same on
     // every path and the compiler never falls back to draining the DMA mid-client.
     auto glds_rows = [&](int k) {
       const __amdgpu_buffer_rsrc_t rr =
           rows_rsrc(q.x + (int64_t)k * q.ld4 * 4, k < q.K ? (uint32_t)(q.P4 * 16) : 0u);
-      const uint32_t slot = (uint32_t)(k % NB) * (QF_V * 64 * 16);
+      const uint32_t slot = (uint32_t)(k % NB) * (QV * 64 * 16);
 #pragma unroll
-      for (int j = 0; j < QF_V; ++j)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rr, (__attribute__((address_space(3))) void*)(uintptr_t)(ldsbase + slot + (uint32_t)(j * 64 * 16)), 16,
-            voff[j], 0, 0, 2);
+      for (int j = 0; j < QV; ++j) rows_load_lds(rr, ldsbase + slot + (uint32_t)(j * 64 * 16), voff[j]);
     };
     // prologue: the first GLDS clients' alphas and slices in flight (alpha before its slice)
     float al_q[NB];
@@ -930,15 +947,10 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else  // (GLDS - 1) x (alpha + 16 slice loads) may stay in flight
           asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
-        f4 t[QF_V];
-        const f4* src = myrow + (kk % NB) * (QF_V * 64);
+        f4 t[QV];
+        const f4* src = myrow + (kk % NB) * (QV * 64);
 #pragma unroll
-        for (int j = 0; j < QF_V; ++j) t[j] = src[64 * j];
-        if constexpr (CLDS) {  // the FedAvg chain of the same upload, in LDS (aggregator.py:500-503)
-          const bool first = (kk == 0) && !(q.flags & FA_ACCUMULATE);
-#pragma unroll
-          for (int j = 0; j < QF_V; ++j) myc[64 * j] = first ? t[j] : myc[64 * j] + t[j];
-        }
+        for (int j = 0; j < QV; ++j) t[j] = src[64 * j];
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // ... and is in registers: refill the slot
         const float al = al_q[0];
 #pragma unroll
@@ -956,17 +968,17 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       const __amdgpu_buffer_rsrc_t grp = rows_rsrc(row0, WIDE ? (uint32_t)nrows * rowbytes : 0u);
 #pragma unroll
       for (int u0 = 0; u0 < QF_G; u0 += QF_U) {
-        f4 t[QF_U][QF_V];
+        f4 t[QF_U][QV];
 #pragma unroll
         for (int u = 0; u < QF_U; ++u) {
           if (WIDE) {
 #pragma unroll
-            for (int j = 0; j < QF_V; ++j) t[u][j] = rows_load(grp, voff[j] + (uint32_t)(u0 + u) * rowbytes);
+            for (int j = 0; j < QV; ++j) t[u][j] = rows_load(grp, voff[j] + (uint32_t)(u0 + u) * rowbytes);
           } else {
             const __amdgpu_buffer_rsrc_t rr =
                 rows_rsrc(row0 + (int64_t)(u0 + u) * q.ld4 * 4, u0 + u < nrows ? (uint32_t)(q.P4 * 16) : 0u);
 #pragma unroll
-            for (int j = 0; j < QF_V; ++j) t[u][j] = rows_load(rr, voff[j]);
+            for (int j = 0; j < QV; ++j) t[u][j] = rows_load(rr, voff[j]);
           }
         }
 #pragma unroll
@@ -1019,10 +1031,10 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
       if ((lane & ((1 << csh) - 1)) == 0 && kg + jcl < q.K) sq[wave][kg + jcl] += y;
     }
 #pragma unroll
-    for (int j = 0; j < QF_V; ++j)
+    for (int j = 0; j < QV; ++j)
       if (ok[j]) {
         reinterpret_cast<f4*>(q.delta)[c0 + 64 * j] = D[j];
-        if (CHAIN) reinterpret_cast<f4*>(q.chain)[c0 + 64 * j] = CLDS ? myc[64 * j] : C[j];
+        if (CHAIN) reinterpret_cast<f4*>(q.chain)[c0 + 64 * j] = C[j];
       }
   }
   __syncthreads();
@@ -1260,8 +1272,16 @@ extern "C" int64_t fa_qfed_workspace_bytes(int32_t K) {  // enough for either ke
 #ifndef QF_PLAIN_GLDS
 #define QF_PLAIN_GLDS 0
 #endif
-#ifndef QF_WIN_COLS
-#define QF_WIN_COLS ((int64_t)QF_GRID * 4 * QF_V * 256)  // one round of full-width tiles (4,194,304 columns); 0: off
+// Tile width (float4 per lane) of the chain launches.  The fused FedAvg chain adds 64 live values per lane;
+// at 16 float4 the LDS-DMA design parks ~200 values in AGPRs (15.0 vs 14.1 ms at 1000 x 25 M), at 12 it
+// parks almost none and runs within 1 % of the plain kernel (round 3: profiles/r03_tune_qfed_chain_width.log).
+// The plain launches keep 16 (the register design at 12 is 10 % slower).  Tiles of another width sum each
+// client's squares in another fp64 order: chain and plain launches' norms agree to ~1e-16 relative.
+#ifndef QF_CHAIN_V
+#define QF_CHAIN_V 12
+#endif
+#ifndef QF_WIN_ROUNDS
+#define QF_WIN_ROUNDS 1  // column windows of this many rounds of full-width tiles (0: no windows)
 #endif
 #ifndef QF_WIDE_BYTES
 #define QF_WIDE_BYTES (1LL << 31)  // largest QF_G-row span served by one descriptor (tuning knob; <= 2^31)
@@ -1269,20 +1289,21 @@ extern "C" int64_t fa_qfed_workspace_bytes(int32_t K) {  // enough for either ke
 static_assert(QF_WIDE_BYTES <= (1LL << 31), "QF_WIDE_BYTES: the rows plus the OOB sentinel must stay below 2^32");
 
 // Column window of one k_qfed_accum launch: per-row descriptors need windows of <= 2^28 columns, and long
-// rows run as windows of one round of full-width tiles (QF_WIN_COLS) — over several rounds of ~1000
+// rows run as windows of one round of full-width tiles (QF_WIN_ROUNDS) — over several rounds of ~1000
 // clients the workgroups drift apart and a launch boundary re-aligns them (tools/tune_qfed2.py,
 // profiles/r02_tune_qfed_windows.log: 1000 x 25 M 6.87 -> 7.03 TB/s, 462 x 100 M 6.34 -> 6.89).  The
 // windows' gathers add their per-client partial norms in window order (deterministic; fp64).
-static int64_t qfed_window(int64_t ld, int64_t P) {
+static int64_t qfed_window(int64_t ld, int64_t P, int qv) {
   const bool wide = (int64_t)ld * 4 * QF_G <= QF_WIDE_BYTES;
   int64_t win = wide ? (P > 0 ? P : 1) : (1LL << 28);
-  if (QF_WIN_COLS > 0 && win > QF_WIN_COLS) win = QF_WIN_COLS;
+  const int64_t cols = (int64_t)QF_WIN_ROUNDS * QF_GRID * 4 * qv * 256;  // rounds of full-width tiles
+  if (cols > 0 && win > cols) win = cols;
   return win;
 }
 
-extern "C" int64_t fa_qfed_launches(int64_t ld, int64_t P) {
+extern "C" int64_t fa_qfed_launches(int64_t ld, int64_t P, int32_t chain) {
   if (P <= 0 || ld < P) return 0;
-  const int64_t win = qfed_window(ld, P);
+  const int64_t win = qfed_window(ld, P, chain ? QF_CHAIN_V : QF_V);
   return (P + win - 1) / win;
 }
 
@@ -1296,7 +1317,8 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
   // WIDE needs QF_G rows plus the sentinel below 2^32; otherwise per-row descriptors over column
   // windows of 2^28 floats (1 GiB), one launch each; the gathers add their partial norms in order.
   const bool wide = (int64_t)ld * 4 * QF_G <= QF_WIDE_BYTES;
-  const int64_t win = qfed_window(ld, P);
+  const int qv = chain ? QF_CHAIN_V : QF_V;
+  const int64_t win = qfed_window(ld, P, qv);
   for (int64_t w0 = 0; w0 < P || w0 == 0; w0 += win) {
     QfArgs qw = q;
     const int64_t pw = P - w0 < win ? P - w0 : win;
@@ -1304,21 +1326,22 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
     qw.P4 = (pw + 3) / 4;
     {  // rounds r = tiles per workgroup at full width; then the narrowest tile that still needs r rounds
       const int64_t S = (qw.P4 + 63) / 64;
-      const int64_t r = (S + (int64_t)QF_GRID * 4 * QF_V - 1) / ((int64_t)QF_GRID * 4 * QF_V);
+      const int64_t r = (S + (int64_t)QF_GRID * 4 * qv - 1) / ((int64_t)QF_GRID * 4 * qv);
       const int64_t strips = r > 0 ? (S + (int64_t)QF_GRID * r - 1) / ((int64_t)QF_GRID * r) : 1;
       qw.sw = (int)((strips + 3) / 4);
       if (qw.sw < 1) qw.sw = 1;
-      if (qw.sw > QF_V || !QF_BALANCE) qw.sw = QF_V;
+      if (qw.sw > qv || !QF_BALANCE) qw.sw = qv;
     }
-    // chain launches: LDS-DMA prefetch (QF_CHAIN_GLDS slices); the plain kernel: register loads
+    // chain launches: LDS-DMA prefetch (QF_CHAIN_GLDS slices) on QF_CHAIN_V-wide tiles; the plain kernel:
+    // register loads on QF_V-wide tiles
     if (wide && chain)
-      hipLaunchKernelGGL((k_qfed_accum<true, true, QF_CHAIN_GLDS>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<true, true, QF_CHAIN_GLDS, QF_CHAIN_V>), dim3(QF_GRID), dim3(256), 0, st, qw);
     else if (wide)
-      hipLaunchKernelGGL((k_qfed_accum<true, false, QF_PLAIN_GLDS>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<true, false, QF_PLAIN_GLDS, QF_V>), dim3(QF_GRID), dim3(256), 0, st, qw);
     else if (chain)
-      hipLaunchKernelGGL((k_qfed_accum<false, true, QF_CHAIN_GLDS>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<false, true, QF_CHAIN_GLDS, QF_CHAIN_V>), dim3(QF_GRID), dim3(256), 0, st, qw);
     else
-      hipLaunchKernelGGL((k_qfed_accum<false, false, QF_PLAIN_GLDS>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<false, false, QF_PLAIN_GLDS, QF_V>), dim3(QF_GRID), dim3(256), 0, st, qw);
     int e = check_launch("fa_qfed_accumulate");
     if (e) return e;
     // the QF_GRID partial rows, summed in a fixed two-level order (16 segments of QF_GRID/16 rows)

