@@ -79,6 +79,9 @@ def parse():
                                                                      "every CPU leg)")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--no-other-configs", action="store_true", help="skip the side measurements (other_configs)")
+    ap.add_argument("--no-selfcheck", action="store_true",
+                    help="N > 1: skip the in-process multi-GPU drop-in check (fedscale_amd.selfcheck) rank 0 runs "
+                         "over all N GPUs after the timed region")
     ap.add_argument("--mem-fraction", type=float, default=0.6,
                     help="share of the free HBM a workload's resident client chunk may take (lower it when several "
                          "ranks share one GPU in a rehearsal)")
@@ -592,6 +595,35 @@ def single_gpu_configs(dev, seed, shards, backend, cpu_budget) -> dict:
     return out
 
 
+def run_selfcheck(world: int, timeout_s: int = 240) -> dict:
+    """fedscale_amd.selfcheck over GPUs 0..N-1 in a child process (rank 0, N > 1): the sharded drop-in against
+    one GPU, bit for bit, with every launch checked against its part's stream.  Summarised for the JSON line."""
+    import subprocess
+
+    import torch
+
+    n = min(world, torch.cuda.device_count())
+    if n < 2:
+        return {"skipped": f"{n} GPU(s) visible to rank 0"}
+    cmd = [sys.executable, "-m", "fedscale_amd.selfcheck", "--devices", ",".join(str(i) for i in range(n))]
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"devices": n, "ok": False, "error": f"no result within {timeout_s} s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if not lines:
+        return {"devices": n, "ok": False, "rc": r.returncode, "error": r.stderr[-400:]}
+    rep = json.loads(lines[-1])
+    out = {"devices": n, "ok": bool(rep.get("ok")), "seconds": round(time.perf_counter() - t0, 1)}
+    if "error" in rep:
+        out["error"] = rep["error"]
+    for pol, v in rep.get("policies", {}).items():
+        out[pol] = {k: v[k] for k in ("ok", "transport", "native_calls", "calls_off_their_stream",
+                                      "buffers_on_their_device", "mismatch") if k in v}
+    return out
+
+
 def main():
     args = parse()
     import numpy as np
@@ -660,6 +692,16 @@ def main():
                 f"c5_qfedavg_k10000_p100M_x{world}": config_line(
                     "c5", CONFIGS["c5"], dev, rank, world, shards, args.seed, args.dist_backend, steps=2, warmup=1)}
 
+    selfcheck = None
+    if world > 1 and not args.no_selfcheck and args.dist_backend == "nccl":
+        # the in-process drop-in (ShardedModelAdapter) over the node's N distinct GPUs, RCCL between them: what a
+        # one-GPU box cannot run.  A child process with a deadline, after every rank has freed its workloads;
+        # the other ranks wait at the barrier.  Outside the timed region; reported, never fatal.
+        _sync_all(dev, world)
+        if rank == 0:
+            selfcheck = run_selfcheck(world)
+        dist.barrier()
+
     if rank == 0:
         ms_per_step = wall * 1e3 / args.steps
         value = (K if strong else world * K) * args.steps / wall
@@ -718,6 +760,8 @@ def main():
                             "roofline_from": "max over ranks of the dominant kernel's mean time per step"}
         if reassembly_ms is not None:
             res["reassembly_ms"] = reassembly_ms
+        if selfcheck is not None:
+            res["inproc_multi_gpu_check"] = selfcheck
         if other is not None:
             res["other_configs"] = other
         if world == 1 and args.cpu_seconds > 0:

@@ -546,3 +546,24 @@ def test_egress_never_mixes_part_versions(gpu_device):
     assert not th.is_alive()
     assert_state_equal(seen["weights"], want[0], "egress during the commit window")
     assert_state_equal(sharded.get_weights(), want[1], "after the round")
+
+
+@pytest.mark.parametrize("devices", ["0", "0,0"])
+def test_selfcheck_module(gpu_device, devices):
+    """fedscale_amd.selfcheck (what bench.py --gpus N runs over the node's N GPUs) on the one-GPU box: a
+    one-GPU RCCL communicator and two parts on one card; every server step bit-identical to one GPU (q-FedAvg
+    within 1e-6), every launch on its part's stream."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "fedscale_amd.selfcheck", "--devices", devices], cwd=root,
+                       capture_output=True, text=True, timeout=300)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines, (r.returncode, r.stderr[-2000:])
+    rep = json.loads(lines[-1])
+    assert r.returncode == 0 and rep["ok"], rep
+    assert set(rep["policies"]) == {"fedavg", "fedbuff", "fed-yogi", "q-fedavg"}
+    assert all(v["calls_off_their_stream"] == 0 and v["native_calls"] > 0 for v in rep["policies"].values())
