@@ -147,6 +147,8 @@ def assert_state_close(got, want, rtol, ctx="", int_slack=0):
         if w.size == 0:
             continue
         if np.issubdtype(w.dtype, np.integer):
+            if int_slack:  # the bound of 1 holds while |v| * rtol < 1 (tests/test_numerics_notes.py)
+                assert np.max(np.abs(w.astype(np.float64))) * max(rtol, 1e-5) < 1, f"{ctx} tensor {i}: int slack"
             assert np.max(np.abs(g.astype(np.int64) - w.astype(np.int64))) <= int_slack, f"{ctx} tensor {i}"
             continue
         wd = w.astype(np.float64)
