@@ -50,6 +50,11 @@ yogi)
 head)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/r3_head_prof -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-other-configs > $OUT/r3_head_prof.log 2>&1 || { tail -20 $OUT/r3_head_prof.log; exit 1; }
   grep '^{' $OUT/r3_head_prof.log | cut -c1-300 ;;
+dist)  # gloo rehearsals (ranks share the one GPU): per-rank kernel times on the N > 1 lines
+  for n in 2 4; do
+    timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 2952$n bench.py --gpus $n --steps 5 --warmup 1 --dist-backend gloo --mem-fraction 0.15 --no-other-configs > $OUT/r3_dist$n.log 2>&1 || { tail -30 $OUT/r3_dist$n.log; exit 1; }
+    grep '^{' $OUT/r3_dist$n.log | cut -c1-200
+  done ;;
 *) echo "unknown stage $STAGE"; exit 2 ;;
 esac
 done
