@@ -390,6 +390,7 @@ class Workload:
                              beta=float(np.float32(0.9)), omb=float(np.float32(1 - 0.9)),
                              omb2=float(np.float32(1 - 0.99)), init=False)
             synth.fill(self.yogi["last"].view(1, -1), 1, self.P, seed=seed + 1)
+            self.mean = torch.zeros(ld, device=dev)  # the round's FedAvg mean (model_weights)
         self.qf = None
         if policy == "qfedavg":
             rng = np.random.default_rng(seed)
@@ -455,8 +456,11 @@ class Workload:
                 kx.reduce(x, n, P, self.acc, a=a, acc_in=acc_in)
             elif self.yogi is None:
                 kx.reduce(x, n, P, self.out, a=a, acc_in=acc_in, denom=self.denom, finalize=True)
-            else:
-                kx.reduce_yogi(x, n, P, out=self.out, a=a, acc_in=acc_in, denom=self.denom, **self.yogi)
+            else:  # as the drop-in runs FedYoGi: the mean, then the YoGi step over it (TorchModelAdapter)
+                kx.reduce(x, n, P, self.mean, a=a, acc_in=acc_in, denom=self.denom, finalize=True)
+                y = self.yogi
+                kx.yogi_step(self.mean, y["last"], y["m"], y["v"], self.out, P, init=y["init"],
+                             **{k: y[k] for k in ("eta", "tau", "beta", "omb", "omb2")})
         if ev is not None:
             ev[1].record(st)
         if self.cmode:  # partial chain of this rank's clients, RCCL all-reduce, finish on the summed vector
@@ -465,13 +469,16 @@ class Workload:
             if self.yogi is None:
                 kx.reduce(x1, 1, P, self.out, denom=self.denom, finalize=True)
             else:
-                kx.reduce_yogi(x1, 1, P, out=self.out, denom=self.denom, **self.yogi)
+                kx.reduce(x1, 1, P, self.mean, denom=self.denom, finalize=True)
+                y = self.yogi
+                kx.yogi_step(self.mean, y["last"], y["m"], y["v"], self.out, P, init=y["init"],
+                             **{k: y[k] for k in ("eta", "tau", "beta", "omb", "omb2")})
 
     def free(self):
         import torch
 
         self.xs = []
-        self.acc = self.out = self.qf = self.yogi = None
+        self.acc = self.out = self.qf = self.yogi = self.mean = None
         torch.cuda.empty_cache()
 
 
@@ -695,6 +702,8 @@ def main():
         launches = n_passes * kx.qfed_launches(w_ld, P_local, chain=w_chain)
     else:
         launches = n_passes * kx.reduce_launches(w.C if n_passes > 1 else K, P_local, weighted=policy == "fedbuff")
+        if policy == "fedyogi":
+            launches += 1  # k_yogi_step after the mean
     w.free()
     del w
 
@@ -766,7 +775,7 @@ def main():
                                     else "k_reduce (fa_reduce, this rank's partial chain)" if w_cmode else
                                     {"fedavg": "k_reduce (fa_reduce FA_FINALIZE)",
                                      "fedbuff": "k_reduce weighted (fa_reduce FA_FINALIZE)",
-                                     "fedyogi": "k_reduce EPI_YOGI (fa_reduce_yogi)"}[policy]),
+                                     "fedyogi": "k_reduce (fa_reduce FA_FINALIZE) + k_yogi_step"}[policy]),
                          "alg_bytes_per_launch": alg_bytes / launches, "launches_per_step": launches,
                          "kernel_ms_per_launch": kern_ms_max / launches},
         }

@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from ...bucket import BucketLayout, ClientStaging
+from ... import kernels as kx
 from ...kernels import qfed_max_chunk as kx_qfed_max_chunk
 from ...round import DeviceRound, default_capacity
 from ...state import DeviceStream, FlatState, ShardGroup
@@ -407,19 +408,21 @@ class TorchModelAdapter(ModelAdapterBase):
             self._finish_qfed(rnd)
             return
         elif mode == "fed-yogi":
+            # the FedAvg mean (aggregator.py:505-507) into its own buffer, then the YoGi step over it
+            # (optimizers.py:43-63, yogi.py:15-36) as a second streaming pass: the same bits as the fused
+            # epilogue (fa_reduce_yogi), 1 % faster at 1000 x 25 M — the fused epilogue's last/m/v traffic sits
+            # at the end of every tile with one wave per SIMD to hide it (tools/yogi_ab.py,
+            # profiles/r03_yogi_fused_vs_unfused.log)
             y = opt.gradient_controller
             y.bind(L, self.device)
-            mean_f = None
-            if keep_mean:
-                if self._mean_f is None or self._mean_f is last.f32 or self._mean_f is out_f:
-                    self._mean_f = torch.zeros(L.ld, dtype=torch.float32, device=self.device)
-                mean_f = self._mean_f
-            yargs = y.fused_args(last.f32)
-            yargs["mean_out"] = mean_f
-            rnd.finalize_mean(denom32, denom64, out=out_f, cur_side=self._mean_s, model_side=None, yogi=yargs)
+            if self._mean_f is None or self._mean_f is last.f32 or self._mean_f is out_f:
+                self._mean_f = torch.zeros(L.ld, dtype=torch.float32, device=self.device)
+            mean_f = self._mean_f
+            rnd.finalize_mean(denom32, denom64, out=mean_f, cur_side=self._mean_s, model_side=None)
+            kx.yogi_step(mean_f, last.f32, y.m, y.v, out_f, L.P, init=not y.initialized, **y.fp32_hparams())
             y.step_side(self._mean_s, last.side, model=out_s)
             y.initialized = True
-            self._mean_valid = keep_mean
+            self._mean_valid = True
         elif mode == "q-fedavg":
             raise RuntimeError("q-fedavg optimizer but the round was not staged as q-FedAvg")
         else:
