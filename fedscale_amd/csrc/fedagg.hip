@@ -740,33 +740,27 @@ __device__ __forceinline__ float fast_div(float a, float b, float r) {
 #ifndef QF_PART
 #define QF_PART 4
 #endif
+#ifndef QF_CHAIN_EMAX
+#define QF_CHAIN_EMAX QF_EMAX  // the bound test of the chain launches (round 3: their own knob)
+#endif
 static_assert(QF_PART == 4 || QF_PART == 8 || QF_PART == 16, "QF_PART: 4, 8 or 16");
+// EMAX picks which bound test admits an element to the fast division; both tests admit only elements the
+// fast division gets correctly rounded, so the choice never changes a bit, only the VALU count.
+template <bool EMAX>
 struct DivRange {
   int emin = 0;  // frexp exponents (0 for +-0): |a| in [2^(e-1), 2^e)
-#if QF_EMAX
   int emax = 0;
-#endif
-#if QF_INFCHK == 1 || !QF_EMAX
-  float amax = 0.f;        // catches +-inf (frexp reports 0 for it)
-#endif
+  float amax = 0.f;  // catches +-inf (frexp reports 0 for it)
   __device__ __forceinline__ void add(float a) {
     const int e = __builtin_amdgcn_frexp_expf(a);
     emin = e < emin ? e : emin;
-#if QF_EMAX
-    emax = e > emax ? e : emax;
-#endif
-#if QF_INFCHK == 1 || !QF_EMAX
-    amax = __builtin_fmaxf(amax, __builtin_fabsf(a));
-#endif
+    if (EMAX) emax = e > emax ? e : emax;
+    if (QF_INFCHK == 1 || !EMAX) amax = __builtin_fmaxf(amax, __builtin_fabsf(a));
   }
   __device__ __forceinline__ bool ok() const {
-#if !QF_EMAX
-    return emin >= -79 && amax < 0x1p80f;
-#elif QF_INFCHK == 1
-    return emin >= -79 && emax <= 80 && amax < __builtin_inff();
-#else
+    if (!EMAX) return emin >= -79 && amax < 0x1p80f;
+    if (QF_INFCHK == 1) return emin >= -79 && emax <= 80 && amax < __builtin_inff();
     return emin >= -79 && emax <= 80;
-#endif
   }
 };
 
@@ -851,7 +845,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
     auto client = [&](f4(&t)[QV], int kk, float al) -> double {
       const bool first = (kk == 0) && !(q.flags & FA_ACCUMULATE);
       f4 g[QV];
-      DivRange rng;
+      DivRange<(CHAIN ? QF_CHAIN_EMAX : QF_EMAX) != 0> rng;
 #pragma unroll
       for (int j = 0; j < QV; ++j) {
         if (CHAIN) C[j] = first ? t[j] : C[j] + t[j];  // the FedAvg chain of the same upload
@@ -1141,7 +1135,7 @@ __global__ __launch_bounds__(64 * QF2_WAVES, 1) void k_qfed_accum2(Qf2Args q) {
 #pragma unroll
         for (int j = 0; j < QF2_V; ++j) t[j] = rows_load(rr, voff[j]);
         const bool first = (k == 0) && !acc_in;
-        DivRange rng;
+        DivRange<QF_EMAX != 0> rng;
 #pragma unroll
         for (int j = 0; j < QF2_V; ++j) {  // pass 1: the FedAvg chain, a = last - W, the range test
           if (CHAIN) C[j] = first ? t[j] : C[j] + t[j];
