@@ -1,6 +1,7 @@
 """Interleaved timing of fa_qfed_accumulate variants (fedscale_amd/variants/libfedagg_qf2_*.so) in one process,
 with and without the fused FedAvg chain.  Every variant's delta (and chain) must equal the first one's bit for bit.
-usage: python tools/tune_qfed2.py [K] [P] [rounds]"""
+usage: python tools/tune_qfed2.py [K] [P] [rounds] [acc]   (acc: time FA_ACCUMULATE launches, a later pass of a
+streamed round: delta and the chain are read back)"""
 import ctypes
 import glob
 import os
@@ -17,6 +18,7 @@ def main():
     K = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
     P = int(sys.argv[2]) if len(sys.argv) > 2 else 25_000_000
     rounds = int(sys.argv[3]) if len(sys.argv) > 3 else 3
+    later = len(sys.argv) > 4 and sys.argv[4] == "acc"
     from fedscale_amd import synth
     from fedscale_amd.bucket import round_up
 
@@ -53,6 +55,8 @@ def main():
                     chain.data_ptr() if use_chain else None, sq.data_ptr(), ws.data_ptr(), 0, st)
             assert f(*args) == 0, n
             torch.cuda.synchronize()
+            if later:  # time later passes: the chains continue from the first call's delta / chain
+                args = args[:11] + (1,) + args[12:]
             if ref is None:
                 ref, ref_sq = delta.clone(), sq.clone()
             else:
@@ -81,7 +85,7 @@ def main():
         kx.reduce(x, K, P, acc)
         assert torch.equal(acc[:P], ref_chain[:P]), "chain != FedAvg sum"
     b = 4 * K * P + 8 * P + 8 * K
-    print(f"--- K={K} P={P} (GB/s over 4KP + 8P + 8K; +chain moves 4P more)")
+    print(f"--- K={K} P={P} {'FA_ACCUMULATE passes ' if later else ''}(GB/s over 4KP + 8P + 8K; +chain moves 4P more)")
     for n, t in sorted(times.items(), key=lambda kv: np.median(kv[1])):
         print(f"{n:40s} {np.median(t):8.3f} ms {b / (np.median(t) * 1e-3) / 1e9:8.1f} GB/s  sqnorm rel {rels.get(n, 0.0):.1e}", flush=True)
 
