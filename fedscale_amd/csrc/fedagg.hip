@@ -1270,16 +1270,21 @@ extern "C" int64_t fa_qfed_workspace_bytes(int32_t K) {  // enough for either ke
 #ifndef QF_PLAIN_GLDS
 #define QF_PLAIN_GLDS 0
 #endif
-// Tile width (float4 per lane) of the chain launches.  The fused FedAvg chain adds 64 live values per lane;
-// at 16 float4 the LDS-DMA design parks ~200 values in AGPRs (15.0 vs 14.1 ms at 1000 x 25 M), at 12 it
-// parks almost none and runs within 1 % of the plain kernel (round 3: profiles/r03_tune_qfed_chain_width.log).
-// The plain launches keep 16 (the register design at 12 is 10 % slower).  Tiles of another width sum each
-// client's squares in another fp64 order: chain and plain launches' norms agree to ~1e-16 relative.
+// Tile width (float4 per lane) of the chain launches.  The fused FedAvg chain adds 4*QV live values per
+// lane; at 16 float4 the LDS-DMA design parks ~200 values in AGPRs (15.0 vs 14.1 ms at 1000 x 25 M).  Round 3
+// measured 4..16 interleaved on three shapes (profiles/r03_tune_qfed_chain_width2.log): 8 is the fastest
+// everywhere (1000 x 25 M and 1024 x 12.5 M at the plain kernel's time, 462 x 100 M 1.5-2 % above it; 12:
+// +2-5 %, 10 and 6: +3-6 %, 4: +25 %).  The plain launches keep 16 (the register design at 12 is 10 %
+// slower, LDS-DMA at 8 mixed: -1 % / +4 % by shape).  Tiles of another width sum each client's squares in
+// another fp64 order: chain and plain launches' norms agree to ~1e-16 relative.
 #ifndef QF_CHAIN_V
-#define QF_CHAIN_V 12
+#define QF_CHAIN_V 8
 #endif
 #ifndef QF_WIN_ROUNDS
 #define QF_WIN_ROUNDS 1  // column windows of this many rounds of full-width tiles (0: no windows)
+#endif
+#ifndef QF_CHAIN_WIN_ROUNDS
+#define QF_CHAIN_WIN_ROUNDS QF_WIN_ROUNDS  // the same for the chain launches
 #endif
 #ifndef QF_WIDE_BYTES
 #define QF_WIDE_BYTES (1LL << 31)  // largest QF_G-row span served by one descriptor (tuning knob; <= 2^31)
@@ -1291,17 +1296,18 @@ static_assert(QF_WIDE_BYTES <= (1LL << 31), "QF_WIDE_BYTES: the rows plus the OO
 // clients the workgroups drift apart and a launch boundary re-aligns them (tools/tune_qfed2.py,
 // profiles/r02_tune_qfed_windows.log: 1000 x 25 M 6.87 -> 7.03 TB/s, 462 x 100 M 6.34 -> 6.89).  The
 // windows' gathers add their per-client partial norms in window order (deterministic; fp64).
-static int64_t qfed_window(int64_t ld, int64_t P, int qv) {
+static int64_t qfed_window(int64_t ld, int64_t P, bool chain) {
   const bool wide = (int64_t)ld * 4 * QF_G <= QF_WIDE_BYTES;
   int64_t win = wide ? (P > 0 ? P : 1) : (1LL << 28);
-  const int64_t cols = (int64_t)QF_WIN_ROUNDS * QF_GRID * 4 * qv * 256;  // rounds of full-width tiles
+  const int64_t qv = chain ? QF_CHAIN_V : QF_V, rounds = chain ? QF_CHAIN_WIN_ROUNDS : QF_WIN_ROUNDS;
+  const int64_t cols = rounds * QF_GRID * 4 * qv * 256;  // rounds of full-width tiles
   if (cols > 0 && win > cols) win = cols;
   return win;
 }
 
 extern "C" int64_t fa_qfed_launches(int64_t ld, int64_t P, int32_t chain) {
   if (P <= 0 || ld < P) return 0;
-  const int64_t win = qfed_window(ld, P, chain ? QF_CHAIN_V : QF_V);
+  const int64_t win = qfed_window(ld, P, chain != 0);
   return (P + win - 1) / win;
 }
 
@@ -1316,7 +1322,7 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
   // windows of 2^28 floats (1 GiB), one launch each; the gathers add their partial norms in order.
   const bool wide = (int64_t)ld * 4 * QF_G <= QF_WIDE_BYTES;
   const int qv = chain ? QF_CHAIN_V : QF_V;
-  const int64_t win = qfed_window(ld, P, qv);
+  const int64_t win = qfed_window(ld, P, chain != nullptr);
   for (int64_t w0 = 0; w0 < P || w0 == 0; w0 += win) {
     QfArgs qw = q;
     const int64_t pw = P - w0 < win ? P - w0 : win;

@@ -5,7 +5,7 @@
 #   c2     config 2 (100 x 1 M, two rotating input sets): rocprofv3 kernel trace + stats, FETCH_SIZE and
 #          WRITE_SIZE passes (MI355X_MICROARCH.md's HBM recipe), per-launch traffic into profiles/pmc_traffic.json
 #   c5     config 5's shard of 8 (10,000 x 12.5 M q-FedAvg, chain launches as the drop-in runs them): kernel
-#          trace + stats, FETCH_SIZE / WRITE_SIZE
+#          trace + stats, FETCH_SIZE / WRITE_SIZE, per-launch traffic into profiles/pmc_traffic.json
 #   yogi   fused FedYoGi at 1000 x 25 M: VALU issue counters, FETCH_SIZE / WRITE_SIZE, kernel trace
 #   head   headline kernel trace + stats (profiles/ summary of this round's library)
 set -o pipefail
@@ -39,7 +39,11 @@ c5)
   grep '^{' $OUT/r3_c5_prof.log | cut -c1-300
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $OUT/r3_c5_$c -o run -- python3 bench.py --config c5 --params 12500000 --steps 1 --warmup 0 --cpu-seconds 0 --no-other-configs > $OUT/r3_c5_$c.log 2>&1 || { tail -5 $OUT/r3_c5_$c.log; exit 1; }
-  done ;;
+  done
+  # per-launch algorithmic bytes and launches per step from the traced run's own bench line
+  AL=$(grep '^{' $OUT/r3_c5_prof.log | tail -1 | python -c "import json,sys; r=json.loads(sys.stdin.read())['roofline']; print(int(r['alg_bytes_per_launch'] * r['launches_per_step']), 'k_qfed_accum', r['launches_per_step'])") || exit 1
+  python tools/pmc_parse.py $OUT/r3_c5_FETCH_SIZE $OUT/r3_c5_WRITE_SIZE qfedavg_k10000_p12500000 $AL > $OUT/r3_c5_pmc.json || exit 1
+  cat $OUT/r3_c5_pmc.json ;;
 yogi)
   ARGS="--policy fedyogi --steps 3 --warmup 1 --cpu-seconds 0 --no-other-configs"
   timeout -s KILL 180 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d $OUT/r3_yogi_valu -o run -- python3 bench.py $ARGS > $OUT/r3_yogi_valu.log 2>&1 || { tail -5 $OUT/r3_yogi_valu.log; exit 1; }
