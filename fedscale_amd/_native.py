@@ -35,6 +35,8 @@ SIGNATURES = {
     "fa_abi_version": (_i32, []),
     "fa_last_error_string": (ctypes.c_char_p, []),
     "fa_reduce": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _f32, _i32, _c_void_p]),
+    "fa_reduce_mirror": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32, _i32,
+                                _c_void_p]),
     "fa_reduce_launches": (_i64, [_i32, _i64, _i32]),
     "fa_qfed_launches": (_i64, [_i64, _i64, _i32]),
     "fa_reduce_yogi": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p,

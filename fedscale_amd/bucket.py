@@ -247,6 +247,9 @@ class ClientStaging:
     #: pinned mirror of the whole area and one H2D per drain() moves all pending rows (small models pay
     #: the per-update copy-enqueue latency otherwise)
     BULK_MAX_BYTES = 64 << 20
+    #: single-chunk rounds of at most this many staged bytes are read by the kernels straight out of the pinned
+    #: mirror (no H2D): at config 1's 1 MB the copy is mostly latency (26.5 us of the 49.8 us device floor)
+    ZERO_COPY_MAX_BYTES = 4 << 20
 
     def __init__(self, layout: BucketLayout, device, capacity: int, ring: int = 2,
                  pack_workers: Optional[int] = None, async_ingress: bool = False, bulk: Optional[bool] = None,
@@ -433,6 +436,24 @@ class ClientStaging:
                 self._bulk_ev.record(torch.cuda.current_stream(self._dev_index))
             self._bulk_busy = True
             self._bulk_lo = self._bulk_hi = 0
+
+    def host_rows(self, n: int):
+        """(x, xi) of the pinned mirror when slots [0, n) were all written since the last drain and are small
+        enough for the round's kernels to read them over PCIe (``ZERO_COPY_MAX_BYTES``): the H2D copy and its
+        latency are skipped (fa_reduce_mirror, tools/c1_zero_copy_probe.py).  None otherwise.  A caller that
+        uses them calls ``release_host_rows()`` after its launches; the device slots [0, n) then stay stale."""
+        if (not self.bulk or self.layout.world != 1 or n <= 0 or self._bulk_lo != 0 or self._bulk_hi != n
+                or n * (self.layout.ld * 4 + self.layout.ldq * 8) > self.ZERO_COPY_MAX_BYTES):
+            return None
+        return self._hx, self._hxi
+
+    def release_host_rows(self):
+        """After the launches that read ``host_rows()``: the mirror's rows are rewritten only once the stream
+        has passed them (the same event as an H2D out of the mirror)."""
+        with self._on():
+            self._bulk_ev.record(torch.cuda.current_stream(self._dev_index))
+        self._bulk_busy = True
+        self._bulk_lo = self._bulk_hi = 0
 
     def drain(self):
         """Wait until every queued copy has been enqueued on its stream (re-raising a copy's error)."""

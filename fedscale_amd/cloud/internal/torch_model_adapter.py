@@ -92,18 +92,20 @@ class _HostBuf:
     __slots__ = ("f", "s", "views")
 
     def __init__(self, layout: BucketLayout):
-        self.f = torch.empty(max(1, layout.P_full), dtype=torch.float32, pin_memory=True)
+        # round_up(P, 4) floats: fa_reduce_mirror writes whole float4 columns into ``f``
+        self.f = torch.empty(max(4, (layout.P_full + 3) // 4 * 4), dtype=torch.float32, pin_memory=True)
         self.s = torch.empty(max(1, layout.Q), dtype=torch.int64)
         self.views = layout.unpack(self.f, self.s)
 
 
 class _HostSnapshot:
-    """One model version's host copy (a ``_HostBuf``) and its reader count."""
+    """One model version's host copy (a ``_HostBuf``) and its reader count.  ``pending``: the round's kernel
+    writes the buffer itself (fa_reduce_mirror) and the first reader waits for the model's ready event."""
 
-    __slots__ = ("version", "buf", "readers")
+    __slots__ = ("version", "buf", "readers", "pending")
 
-    def __init__(self, version, buf: _HostBuf):
-        self.version, self.buf, self.readers = version, buf, 0
+    def __init__(self, version, buf: _HostBuf, pending: bool = False):
+        self.version, self.buf, self.readers, self.pending = version, buf, 0, pending
 
 
 def _resolve_device(device) -> torch.device:
@@ -180,12 +182,32 @@ class TorchModelAdapter(ModelAdapterBase):
     def _scratch_buffers(self):
         return self._f[1 - self._cur], self._s[1 - self._cur]
 
-    def _commit_scratch(self):
+    def _commit_scratch(self, host: Optional[_HostBuf] = None):
+        """Make the scratch buffers the model.  ``host``: a pinned buffer the round's kernel is writing the new
+        model into (fa_reduce_mirror); it becomes the new version's egress snapshot, so egress needs no D2H."""
         self._ready_stream = self.dstream.stream  # every write to the model buffers is issued on it
         self._ready.record(self._ready_stream)
         with self._egress_lock:  # (buffer, version) flip atomically for the servicer threads
             self._cur = 1 - self._cur
             self._version += 1
+            if host is not None:
+                old, self._snap = self._snap, _HostSnapshot(self._version, host, pending=True)
+                if old is not None and old.readers == 0:
+                    self._snap_pool.append(old.buf)
+
+    #: FedAvg / FedBuff rounds of models of at most this many fp32 bytes (and no int64 entries) write the new
+    #: model into its egress snapshot from the reduce's epilogue (fa_reduce_mirror): no D2H, no copy stream
+    EGRESS_MIRROR_MAX_BYTES = 4 << 20
+
+    def _mirror_target(self) -> Optional[_HostBuf]:
+        """A free pinned snapshot buffer for fa_reduce_mirror, when this adapter's rounds qualify."""
+        L = self.layout
+        if L.world != 1 or L.Q or self.shards.world != 1 or L.P_full * 4 > self.EGRESS_MIRROR_MAX_BYTES:
+            return None
+        with self._egress_lock:
+            if self._snap_pool:
+                return self._snap_pool.pop()
+        return _HostBuf(L)  # allocated with this adapter's GPU current (inside its DeviceStream)
 
     def _sqnorm_allreduce(self):
         return self.shards.sum_partials if self.shards.shards_params else None
@@ -253,6 +275,9 @@ class TorchModelAdapter(ModelAdapterBase):
         it change (aggregator.py:788-804, 902-909 read the model from up to 20 servicer threads)."""
         with self._egress_lock:
             snap = self._snap
+            if snap is not None and snap.pending and snap.version == self._version:
+                self._ready.synchronize()  # the round's kernel wrote this snapshot (fa_reduce_mirror)
+                snap.pending = False
             if snap is None or snap.version != self._version:
                 buf = self._snap_pool.pop() if self._snap_pool else _HostBuf(self.layout)
                 self._copy_to_host(buf.f, buf.s)
@@ -426,9 +451,13 @@ class TorchModelAdapter(ModelAdapterBase):
         elif mode == "q-fedavg":
             raise RuntimeError("q-fedavg optimizer but the round was not staged as q-FedAvg")
         else:
-            rnd.finalize_mean(denom32, denom64, out=out_f, cur_side=self._mean_s, model_side=out_s)
+            host = self._mirror_target()
+            rnd.finalize_mean(denom32, denom64, out=out_f, cur_side=self._mean_s, model_side=out_s,
+                              mirror=None if host is None else host.f)
             self._mean_f = out_f  # FedAvg without a server step: the mean IS the new model
             self._mean_valid = True
+            self._commit_scratch(host)
+            return
         self._commit_scratch()
 
     def _finish_qfed(self, rnd: DeviceRound):

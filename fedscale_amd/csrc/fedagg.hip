@@ -238,6 +238,7 @@ __device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int 
       o.z = __fdiv_rn(s[j].z, r.denom);
       o.w = __fdiv_rn(s[j].w, r.denom);
       reinterpret_cast<f4*>(r.out)[c] = o;
+      if (r.mean_out) reinterpret_cast<f4*>(r.mean_out)[c] = o;  // fa_reduce_mirror (may be pinned host)
     } else {  // EPI_YOGI
       const f4 L = reinterpret_cast<const f4*>(r.last)[c];
       f4 M, Vv;
@@ -602,6 +603,21 @@ extern "C" int fa_reduce(const float* x, int64_t ld, int32_t K, int64_t P, const
   hipStream_t st = (hipStream_t)stream;
   if (flags & FA_FINALIZE) return launch_reduce<EPI_MEAN>(r, st, "fa_reduce");
   return launch_reduce<EPI_CHAIN>(r, st, "fa_reduce");
+}
+
+extern "C" int fa_reduce_mirror(const float* x, int64_t ld, int32_t K, int64_t P, const float* a,
+                                const float* acc_in, float* out, float* mirror, float denom, int32_t flags,
+                                fa_stream_t stream) {
+  int e = check_reduce_args("fa_reduce_mirror", x, ld, K, P, acc_in, out, flags);
+  if (e) return e;
+  if (!(flags & FA_FINALIZE)) return fail(FA_E_ARG, "fa_reduce_mirror: needs FA_FINALIZE");
+  if (!mirror || !aligned16(mirror)) return fail(FA_E_ARG, "fa_reduce_mirror: mirror NULL or not 16-byte aligned");
+  if (P == 0) return FA_OK;
+  RedArgs r{};
+  r.x = x; r.ld4 = ld / 4; r.P4 = (P + 3) / 4; r.K = K; r.flags = flags; r.a = a; r.acc_in = acc_in;
+  r.out = out; r.denom = denom; r.mean_out = mirror;
+  FA_DEVICE_SCOPE("fa_reduce_mirror", stream, out);
+  return launch_reduce<EPI_MEAN>(r, (hipStream_t)stream, "fa_reduce_mirror");
 }
 
 extern "C" int fa_reduce_yogi(const float* x, int64_t ld, int32_t K, int64_t P, const float* a,

@@ -38,8 +38,21 @@ def _stream(t: torch.Tensor):
     return raw_stream(t.device.index)
 
 
-def _check_x(x: torch.Tensor, K: int, P: int):
-    _dev(x, torch.float32, "x")
+def _pinned(t: torch.Tensor, dtype, name: str, min_numel: int = 0):
+    """A page-locked host tensor a kernel may read or write over PCIe (fa_reduce_mirror's host operands)."""
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected a torch.Tensor, got {type(t).__name__}")
+    if t.device.type != "cpu" or not t.is_pinned():
+        raise ValueError(f"{name}: a host operand must be pinned (page-locked) memory")
+    if t.dtype != dtype or not t.is_contiguous() or t.numel() < min_numel or t.data_ptr() % 16:
+        raise ValueError(f"{name}: needs a contiguous, 16-byte aligned {dtype} buffer of >= {min_numel} elements")
+
+
+def _check_x(x: torch.Tensor, K: int, P: int, host_ok: bool = False):
+    if host_ok and isinstance(x, torch.Tensor) and x.device.type == "cpu":
+        _pinned(x, torch.float32, "x")
+    else:
+        _dev(x, torch.float32, "x")
     if x.dim() != 2:
         raise ValueError("x: expected a [K, ld] client-major buffer")
     if K > x.shape[0]:
@@ -51,9 +64,11 @@ def _check_x(x: torch.Tensor, K: int, P: int):
 
 
 def reduce(x: torch.Tensor, K: int, P: int, out: torch.Tensor, *, a: Optional[torch.Tensor] = None,
-           acc_in: Optional[torch.Tensor] = None, denom: float = 1.0, finalize: bool = False) -> torch.Tensor:
-    """In-order weighted column reduction of x[:K, :P] (fa_reduce)."""
-    ld = _check_x(x, K, P) if K > 0 else (x.shape[1] if x is not None else _cols(P))
+           acc_in: Optional[torch.Tensor] = None, denom: float = 1.0, finalize: bool = False,
+           host_ok: bool = False) -> torch.Tensor:
+    """In-order weighted column reduction of x[:K, :P] (fa_reduce); ``host_ok``: x may be a pinned host
+    tensor, read by the kernel over PCIe."""
+    ld = _check_x(x, K, P, host_ok) if K > 0 else (x.shape[1] if x is not None else _cols(P))
     _dev(out, torch.float32, "out", _cols(P))
     if a is not None:
         _dev(a, torch.float32, "a", K, align=4)
@@ -62,6 +77,27 @@ def reduce(x: torch.Tensor, K: int, P: int, out: torch.Tensor, *, a: Optional[to
     flags = (FA_ACCUMULATE if acc_in is not None else 0) | (FA_FINALIZE if finalize else 0)
     call("fa_reduce", ptr(x) if K > 0 else None, ld, K, P, ptr(a), ptr(acc_in), ptr(out), float(denom), flags,
          _stream(out))
+    return out
+
+
+def reduce_mirror(x: torch.Tensor, K: int, P: int, out: torch.Tensor, mirror: torch.Tensor, *,
+                  a: Optional[torch.Tensor] = None, acc_in: Optional[torch.Tensor] = None,
+                  denom: float = 1.0) -> torch.Tensor:
+    """The finalizing reduce (fa_reduce_mirror) with the mean written to ``out`` and to ``mirror``; ``x`` and
+    ``mirror`` may be pinned host tensors (the kernel reads / writes them over PCIe)."""
+    ld = _check_x(x, K, P, host_ok=True) if K > 0 else _cols(P)
+    _dev(out, torch.float32, "out", _cols(P))
+    if mirror.device.type == "cpu":
+        _pinned(mirror, torch.float32, "mirror", _cols(P))
+    else:
+        _dev(mirror, torch.float32, "mirror", _cols(P))
+    if a is not None:
+        _dev(a, torch.float32, "a", K, align=4)
+    if acc_in is not None:
+        _dev(acc_in, torch.float32, "acc_in", _cols(P))
+    flags = (FA_ACCUMULATE if acc_in is not None else 0) | FA_FINALIZE
+    call("fa_reduce_mirror", ptr(x) if K > 0 else None, ld, K, P, ptr(a), ptr(acc_in), ptr(out), ptr(mirror),
+         float(denom), flags, _stream(out))
     return out
 
 
@@ -158,9 +194,13 @@ def sum_rows_f64(x: torch.Tensor, out: torch.Tensor):
 
 # ---- side table (int64 entries) ---------------------------------------------------------------
 def side_accumulate(xi, K, Q, mode, *, w=None, acc_i=None, acc_d=None, accumulate=False):
+    """``xi`` may be a pinned host tensor (the staging mirror): the kernel then reads it over PCIe."""
     if Q == 0 or K == 0:
         return
-    _dev(xi, torch.int64, "xi", align=8)
+    if xi.device.type == "cpu":
+        _pinned(xi, torch.int64, "xi")
+    else:
+        _dev(xi, torch.int64, "xi", align=8)
     ldq = xi.shape[1]
     if mode == 0:
         _dev(acc_i, torch.int64, "acc_i", Q, align=8)
@@ -168,7 +208,7 @@ def side_accumulate(xi, K, Q, mode, *, w=None, acc_i=None, acc_d=None, accumulat
         _dev(acc_d, torch.float64, "acc_d", Q, align=8)
         _dev(w, torch.float64, "w", K, align=8)
     call("fa_side_accumulate", ptr(xi), ldq, K, Q, mode, ptr(w), ptr(acc_i), ptr(acc_d),
-         FA_ACCUMULATE if accumulate else 0, _stream(xi))
+         FA_ACCUMULATE if accumulate else 0, _stream(acc_i if mode == 0 else acc_d))
 
 
 def side_close(Q, mode, denom, *, acc_i=None, acc_d=None, cur=None, model=None):

@@ -242,30 +242,42 @@ class DeviceRound:
     # ---- FedAvg / FedBuff: mean (+ optional fused FedYoGi) --------------------------------------
     @on_stream
     def finalize_mean(self, denom32: float, denom64: float, *, out: torch.Tensor, cur_side: torch.Tensor,
-                      model_side: Optional[torch.Tensor] = None, yogi: Optional[dict] = None):
+                      model_side: Optional[torch.Tensor] = None, yogi: Optional[dict] = None,
+                      mirror: Optional[torch.Tensor] = None):
         """Reduce the last chunk with the epilogue fused.
 
         out        <- fp32 mean (or, with ``yogi``, the new global model last + step)
         cur_side   <- float64 mean of the side table (np.divide of int64 sums)
         model_side <- int64(fp32(mean)) (what load_state_dict stores), when given
         yogi       -> dict(last=, m=, v=, eta=, tau=, beta=, omb=, omb2=, init=)
-        """
+        mirror     <- (no ``yogi``) a second copy of the mean, e.g. a pinned host buffer (fa_reduce_mirror)
+
+        A small single-chunk round whose updates are all still in the staging's pinned mirror is reduced
+        straight from it (``ClientStaging.host_rows``): no H2D copy."""
         self._check_complete()
-        self.staging.drain()
         if self.cg is not None:
+            self.staging.drain()
             return self._finalize_mean_clients(denom32, denom64, out, cur_side, model_side, yogi)
         L, st, n = self.layout, self.staging, self.slot
         first = self.chunks_done == 0
+        zc = st.host_rows(n) if (first and yogi is None) else None
+        if zc is None:
+            st.drain()
+        x, xi = zc if zc is not None else (st.x, st.xi)
         a32 = a64 = None
         if self.policy == "fedbuff":
             a32, a64 = self._chunk_weights()
         acc_in = None if first else self.acc
-        if yogi is None:
-            kx.reduce(st.x, n, L.P, out, a=a32, acc_in=acc_in, denom=denom32, finalize=True)
+        if yogi is not None:
+            kx.reduce_yogi(x, n, L.P, a=a32, acc_in=acc_in, denom=denom32, out=out, **yogi)
+        elif mirror is not None:
+            kx.reduce_mirror(x, n, L.P, out, mirror, a=a32, acc_in=acc_in, denom=denom32)
         else:
-            kx.reduce_yogi(st.x, n, L.P, a=a32, acc_in=acc_in, denom=denom32, out=out, **yogi)
+            kx.reduce(x, n, L.P, out, a=a32, acc_in=acc_in, denom=denom32, finalize=True, host_ok=zc is not None)
         mode = 0 if self.policy == "fedavg" else 1
-        kx.side_accumulate(st.xi, n, L.Q, mode, w=a64, acc_i=self.acc_i, acc_d=self.acc_d, accumulate=not first)
+        kx.side_accumulate(xi, n, L.Q, mode, w=a64, acc_i=self.acc_i, acc_d=self.acc_d, accumulate=not first)
+        if zc is not None:
+            st.release_host_rows()
         kx.side_close(L.Q, mode, denom64, acc_i=self.acc_i, acc_d=self.acc_d, cur=cur_side, model=model_side)
 
     @on_stream

@@ -67,6 +67,19 @@ int fa_reduce(const float* x, int64_t ld, int32_t K, int64_t P, const float* a, 
               float* out, float denom, int32_t flags, fa_stream_t stream);
 
 /*
+ * fa_reduce with FA_FINALIZE whose epilogue writes the mean twice: into out (device, the new global model)
+ * and into `mirror` (round_up(P, 4) floats), which may be PINNED HOST memory (page-locked, mapped for the
+ * GPU of `out`).  `x` may be pinned host memory too: the kernel then reads the client rows over PCIe.
+ * For small rounds (config 1: 10 x 24,492) this replaces H2D + reduce + D2H with one launch
+ * (tools/c1_zero_copy_probe.py: 49.8 -> 31.9 us on the device); the arithmetic and its order are fa_reduce's.
+ * Replaces: the same lines as fa_reduce (aggregator.py:489-511, async_aggregator.py:115-137) followed by
+ *           get_weights()'s copy of the model to the host (torch_model_adapter.py:41-47).
+ * Host buffers are visible to the host once the stream has passed the launch (an event or a synchronize).
+ */
+int fa_reduce_mirror(const float* x, int64_t ld, int32_t K, int64_t P, const float* a, const float* acc_in,
+                     float* out, float* mirror, float denom, int32_t flags, fa_stream_t stream);
+
+/*
  * Number of kernel launches one fa_reduce (or fa_reduce_yogi) call makes at (K, P) on the current device:
  * long buckets run as several launches over column windows.  For reporting per-launch figures (bench.py);
  * no reference counterpart.  Needs a GPU (the plan depends on the CU count).

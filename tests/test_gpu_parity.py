@@ -50,15 +50,20 @@ def _device_run(sc, capacity=None):
         yield r, adapter, opt, agg
 
 
-@pytest.mark.parametrize("bulk", [True, False], ids=["bulk", "perupdate"])
+@pytest.mark.parametrize("bulk", ["zerocopy", "bulk", "perupdate"])
 @pytest.mark.parametrize("capacity", [None, 2])
 @pytest.mark.parametrize("name", scenario_names())
 def test_device_path_matches_reference_fixture(gpu_device, name, capacity, bulk, monkeypatch):
-    """Every fixture through the device path, with the small-model bulk staging (one H2D per drain) and
-    with the per-update H2D ring that large models use."""
+    """Every fixture through the device path: small single-chunk rounds read the pinned mirror and write the
+    egress snapshot from the kernel (zerocopy, the default for small models), the small-model bulk staging
+    with one H2D per drain and a D2H for egress (bulk), and the per-update H2D ring of large models."""
     from fedscale_amd.bucket import ClientStaging
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
 
-    monkeypatch.setattr(ClientStaging, "BULK_MAX_BYTES", ClientStaging.BULK_MAX_BYTES if bulk else -1)
+    monkeypatch.setattr(ClientStaging, "BULK_MAX_BYTES", ClientStaging.BULK_MAX_BYTES if bulk != "perupdate" else -1)
+    if bulk != "zerocopy":
+        monkeypatch.setattr(ClientStaging, "ZERO_COPY_MAX_BYTES", -1)
+        monkeypatch.setattr(TorchModelAdapter, "EGRESS_MIRROR_MAX_BYTES", -1)
     sc = Scenario(name)
     for r, adapter, opt, agg in _device_run(sc, capacity):
         got = adapter.get_weights()

@@ -116,7 +116,7 @@ def test_sharded_equals_single_gpu(gpu_device, name):
 
 
 #: entry points that enqueue GPU work (their last argument is the stream, or the per-device stream table)
-LAUNCHES = {"fa_reduce", "fa_reduce_yogi", "fa_yogi_step", "fa_qfed_accumulate", "fa_qfed_hs", "fa_qfed_finalize",
+LAUNCHES = {"fa_reduce", "fa_reduce_mirror", "fa_reduce_yogi", "fa_yogi_step", "fa_qfed_accumulate", "fa_qfed_hs", "fa_qfed_finalize",
             "fa_sum_rows_f64", "fa_side_accumulate", "fa_side_close", "fa_side_yogi", "fa_side_qfed_accumulate",
             "fa_side_qfed_finalize", "fa_fill_synthetic", "fa_prefix_box_combine", "fa_rccl_all_gather",
             "fa_rccl_all_reduce", "fa_rccl_gather", "fa_rccl_broadcast"}

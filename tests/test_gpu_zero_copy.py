@@ -1,0 +1,192 @@
+"""Small rounds read the staged updates out of the pinned mirror and write the new model into its egress
+snapshot (fa_reduce_mirror).  Same arithmetic and order as fa_reduce, so every result
+is bit-exact against the oracle; the tests also pin down which buffers the kernels actually touched and that
+a snapshot a reader holds never changes under it."""
+import numpy as np
+import pytest
+import torch
+
+from oracle.cpu_reference import fedavg_close, fedavg_flat, fedavg_step, fedbuff_flat
+from tests.golden_io import StateDictModule, assert_state_equal
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("K,P", [(10, 24492), (3, 5), (64, 1001), (1, 4096)])
+@pytest.mark.parametrize("x_host", [True, False], ids=["x_pinned", "x_device"])
+@pytest.mark.parametrize("mirror_host", [True, False], ids=["mirror_pinned", "mirror_device"])
+def test_reduce_mirror_bit_exact(gpu_device, K, P, x_host, mirror_host):
+    from fedscale_amd import kernels as kx
+
+    ld = (P + 63) // 64 * 64
+    rng = np.random.default_rng(K * 7 + P)
+    xh = torch.from_numpy(rng.standard_normal((K, ld), dtype=np.float32))
+    xh[:, P:] = 0
+    x = xh.pin_memory() if x_host else xh.to(gpu_device)
+    out = torch.full((ld,), np.nan, device=gpu_device)
+    mirror = torch.full((ld,), np.nan).pin_memory() if mirror_host else torch.full((ld,), np.nan, device=gpu_device)
+    a = torch.from_numpy(rng.uniform(0.2, 1.0, K).astype(np.float32)).to(gpu_device)
+    kx.reduce_mirror(x, K, P, out, mirror, denom=float(np.float32(K)))
+    torch.cuda.synchronize()
+    want = fedavg_flat(xh[:K, :P].numpy())
+    assert np.array_equal(out[:P].cpu().numpy(), want)
+    assert np.array_equal(mirror[:P].cpu().numpy(), want)
+    # weighted (FedBuff) form, same buffers
+    s = a.cpu().numpy()
+    den = float(np.float32(sum(float(v) for v in s)))
+    kx.reduce_mirror(x, K, P, out, mirror, a=a, denom=den)
+    torch.cuda.synchronize()
+    ref = torch.empty(ld, device=gpu_device)
+    kx.reduce(xh.to(gpu_device), K, P, ref, a=a, denom=den, finalize=True)
+    torch.cuda.synchronize()
+    assert torch.equal(out[:P], ref[:P]) and torch.equal(mirror[:P].cpu(), ref[:P].cpu())
+
+
+def test_reduce_mirror_rejects_pageable_host_memory(gpu_device):
+    from fedscale_amd import kernels as kx
+
+    x = torch.zeros(2, 64)  # pageable: the kernel must never be handed it
+    out = torch.zeros(64, device=gpu_device)
+    with pytest.raises(ValueError, match="pinned"):
+        kx.reduce_mirror(x, 2, 64, out, torch.zeros(64).pin_memory())
+    with pytest.raises(ValueError, match="pinned"):
+        kx.reduce_mirror(x.to(gpu_device), 2, 64, out, torch.zeros(64))
+
+
+def _femnist_adapter(gpu_device, extra_int=False):
+    from fedscale_amd import synth
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    names, shapes, _ = synth.femnist_cnn_layout()
+    g = torch.Generator().manual_seed(3)
+    tensors = [torch.randn(s, generator=g) * 0.05 for s in shapes]
+    if extra_int:
+        names, tensors = names + ["bn.num_batches_tracked"], tensors + [torch.tensor(5)]
+    adapter = TorchModelAdapter(StateDictModule(names, tensors), device=gpu_device)
+    return names, tensors, adapter, DeviceAggregator(adapter)
+
+
+def _uploads(names, tensors, K, seed):
+    rng = np.random.default_rng(seed)
+    ups = []
+    for _ in range(K):
+        u = {}
+        for n, t in zip(names, tensors):
+            a = t.numpy()
+            u[n] = (np.asarray(a + int(rng.integers(0, 7)), dtype=np.int64) if a.dtype == np.int64 else
+                    (a + rng.standard_normal(a.shape).astype(np.float32) * np.float32(0.01)).astype(np.float32))
+        ups.append(u)
+    return ups
+
+
+def _spy(monkeypatch):
+    from fedscale_amd import _native
+    from fedscale_amd import kernels as kx
+
+    calls, real = [], _native.call
+
+    def spy(fn, *args):
+        calls.append((fn, args))
+        return real(fn, *args)
+
+    monkeypatch.setattr(_native, "call", spy)
+    monkeypatch.setattr(kx, "call", spy)
+    return calls
+
+
+def _oracle_round(ups):
+    acc = None
+    for k, u in enumerate(ups):
+        acc = fedavg_step(acc, u, k == 0)
+    return fedavg_close(acc, len(ups))
+
+
+def test_config1_rounds_read_the_mirror_and_write_egress(gpu_device, monkeypatch):
+    """Config 1's shape (10 x 24,492): the reduce reads the staging's pinned mirror and writes the new model
+    into the egress snapshot; no H2D of the rows, no D2H of the model; get_weights bit-exact every round, and
+    a snapshot held across the next round keeps its version's values."""
+    names, tensors, adapter, agg = _femnist_adapter(gpu_device)
+    calls = _spy(monkeypatch)
+    held = None
+    for r in range(4):
+        ups = _uploads(names, tensors, 10, r)
+        del calls[:]
+        agg.start_round(10)
+        for k, u in enumerate(ups):
+            agg.on_result({"client_id": k, "update_weight": u, "moving_loss": 1.0})
+        mir = [c for c in calls if c[0] == "fa_reduce_mirror"]
+        assert len(mir) == 1 and not [c for c in calls if c[0] == "fa_reduce"], [c[0] for c in calls]
+        assert mir[0][1][0] == adapter.staging._hx.data_ptr(), "the reduce did not read the pinned mirror"
+        assert mir[0][1][7] == adapter._snap.buf.f.data_ptr(), "the mean was not written into the snapshot"
+        want = _oracle_round(ups)
+        assert_state_equal(adapter.get_weights(), want, f"round {r}")
+        assert_state_equal(list(agg.model_weights), want, f"model_weights round {r}")
+        if held is not None:  # the previous version's snapshot, held by a reader through this round
+            snap, prev = held
+            assert_state_equal([v.clone() for v in snap.buf.views], prev, f"held snapshot of round {r - 1}")
+            adapter._release_host(snap)
+        held = (adapter._acquire_host(), want)
+    adapter._release_host(held[0])
+    # set_weights (no round kernel) falls back to the D2H snapshot and stays exact
+    new = [np.asarray(t.numpy() * 2, dtype=np.float32) for t in tensors]
+    adapter.set_weights(new)
+    assert_state_equal(adapter.get_weights(), new, "after set_weights")
+
+
+def test_int64_entries_read_from_the_mirror_without_egress_mirror(gpu_device, monkeypatch):
+    """A model with an int64 entry: the rows (fp32 bucket and side table) are still read from the pinned
+    mirror, the egress takes the D2H path; bit-exact."""
+    names, tensors, adapter, agg = _femnist_adapter(gpu_device, extra_int=True)
+    calls = _spy(monkeypatch)
+    for r in range(2):
+        ups = _uploads(names, tensors, 6, 10 + r)
+        del calls[:]
+        agg.start_round(6)
+        for k, u in enumerate(ups):
+            agg.on_result({"client_id": k, "update_weight": u, "moving_loss": 1.0})
+        red = [c for c in calls if c[0] == "fa_reduce"]
+        side = [c for c in calls if c[0] == "fa_side_accumulate"]
+        assert len(red) == 1 and red[0][1][0] == adapter.staging._hx.data_ptr()
+        assert len(side) == 1 and side[0][1][0] == adapter.staging._hxi.data_ptr()
+        want = _oracle_round(ups)
+        got = adapter.get_weights()
+        assert_state_equal(got[:-1], want[:-1], f"round {r}")
+        # load_state_dict of np.asarray(mean, float32) into the int64 entry truncates (torch_model_adapter.py:31-35)
+        assert int(got[-1]) == int(np.float32(want[-1])), f"round {r} int64 entry"
+
+
+def test_fedbuff_small_round_from_the_mirror(gpu_device):
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAsyncAggregator
+
+    names, tensors, adapter, _ = _femnist_adapter(gpu_device)
+    agg = DeviceAsyncAggregator(adapter)
+    agg.round = 9
+    ups = _uploads(names, tensors, 8, 77)
+    for k in range(8):
+        agg.client_task_model_version[k] = agg.round - k % 5
+    agg.start_round(8)
+    for k, u in enumerate(ups):
+        agg.on_result({"client_id": k, "update_weight": u, "moving_loss": 1.0})
+    s = [1 / (1 + (k % 5)) ** 0.5 for k in range(8)]
+    got = adapter.get_weights()
+    for i in range(len(names)):
+        x = np.stack([u[names[i]].reshape(-1) for u in ups])
+        assert np.array_equal(got[i].numpy().reshape(-1), fedbuff_flat(x, s)), names[i]
+
+
+def test_chunked_small_round_keeps_the_h2d_path(gpu_device, monkeypatch):
+    """A round that folds a chunk first (capacity < K) reduces its last chunk from the device slots."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+
+    names, tensors, adapter, _ = _femnist_adapter(gpu_device)
+    agg = DeviceAggregator(adapter)
+    agg.device_round_capacity = 4
+    calls = _spy(monkeypatch)
+    ups = _uploads(names, tensors, 10, 5)
+    agg.start_round(10)
+    for k, u in enumerate(ups):
+        agg.on_result({"client_id": k, "update_weight": u, "moving_loss": 1.0})
+    mir = [c for c in calls if c[0] == "fa_reduce_mirror"]
+    assert len(mir) == 1 and mir[0][1][0] == adapter.staging.x.data_ptr()
+    assert_state_equal(adapter.get_weights(), _oracle_round(ups), "chunked")
