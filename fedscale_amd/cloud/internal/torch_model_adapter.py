@@ -89,13 +89,14 @@ class _HostBuf:
     """Pinned host buffers for one model version (fp32 bucket ``f``, side table ``s``) with their state_dict
     views, made once: buffers are pooled across versions, so egress clones from ready-made views."""
 
-    __slots__ = ("f", "s", "views")
+    __slots__ = ("f", "s", "views", "np_views")
 
     def __init__(self, layout: BucketLayout):
         # round_up(P, 4) floats: fa_reduce_mirror writes whole float4 columns into ``f``
         self.f = torch.empty(max(4, (layout.P_full + 3) // 4 * 4), dtype=torch.float32, pin_memory=True)
         self.s = torch.empty(max(1, layout.Q), dtype=torch.int64)
         self.views = layout.unpack(self.f, self.s)
+        self.np_views = [v.numpy() for v in self.views]
 
 
 class _HostSnapshot:
@@ -295,7 +296,9 @@ class TorchModelAdapter(ModelAdapterBase):
                 self._snap_pool.append(snap.buf)
 
     def _clone_weights(self, snap: "_HostSnapshot") -> list:
-        return [t.clone() for t in snap.buf.views]
+        # the reference's params.data.clone() per entry (torch_model_adapter.py:47): a fresh CPU tensor each,
+        # copied through numpy (half the per-tensor cost of Tensor.clone on small models)
+        return [torch.from_numpy(a.copy()) for a in snap.buf.np_views]
 
     def get_weights(self) -> List[torch.Tensor]:
         """torch_model_adapter.py:41-47: cloned CPU tensors in state_dict order (gathers the shards).

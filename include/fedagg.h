@@ -147,7 +147,8 @@ int fa_qfed_finalize(const float* last, const float* delta, const float* hs_dev,
 
 /*
  * Side table (non-fp32 state_dict entries, BatchNorm num_batches_tracked etc.).
- * xi: device int64 [K][Q] client-major.  State: acc_i (int64 [Q]) and acc_d (fp64 [Q]).
+ * xi: int64 [K][Q] client-major, device or pinned host memory (read over PCIe: small rounds read the staging's
+ *     pinned mirror, as fa_reduce_mirror does).  State: acc_i (int64 [Q]) and acc_d (fp64 [Q]).
  *   mode 0 FedAvg : acc_i = acc_i + xi[k]  (int64, aggregator.py:500-503)
  *   mode 1 FedBuff: acc_d = acc_d + w[k]*double(xi[k]), first = double(xi[0])*w[0] (async_aggregator.py:129-133)
  * w: device fp64[K] or NULL.  FA_ACCUMULATE continues a previous chunk.
