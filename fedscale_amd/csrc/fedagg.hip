@@ -436,9 +436,14 @@ static void launch_balanced(RedArgs r, int64_t sw, int64_t rounds, hipStream_t s
 
 // One round of tiles over the column window [s0, s0 + ns) strips (64 float4 columns each) on about `cap`
 // workgroups: the kernel's col0 / P4 bound the window, outputs stay indexed by absolute column.
+#ifndef FA_WIN_FULL_MIN
+#define FA_WIN_FULL_MIN 33  // tuning knob: windows whose tiles would be >= this many strips wide take full 32-wide
+                            // tiles on fewer workgroups instead (33: off)
+#endif
 template <int EPI, bool W>
 static void launch_window(RedArgs r, int64_t s0, int64_t ns, int64_t cap, hipStream_t st) {
-  const int64_t sw = (ns + (int64_t)FA_RED_WAVES * cap - 1) / ((int64_t)FA_RED_WAVES * cap);
+  int64_t sw = (ns + (int64_t)FA_RED_WAVES * cap - 1) / ((int64_t)FA_RED_WAVES * cap);
+  if (sw >= FA_WIN_FULL_MIN && sw < 32) sw = 32;
   r.col0 = s0 * 64;
   r.P4 = (s0 + ns) * 64 < r.P4 ? (s0 + ns) * 64 : r.P4;
   r.sw = (int)sw;
