@@ -81,6 +81,23 @@ __device__ __forceinline__ f4 ldnt(const f4* p) {
 #endif
 }
 
+#ifndef FA_RED_BUF
+#define FA_RED_BUF 0  // tuning: 1 = k_reduce reads client rows with raw buffer loads of cache policy FA_RED_AUX
+#endif
+#ifndef FA_RED_AUX
+#define FA_RED_AUX 2  // buffer-load cache policy bits (gfx950: 1 sc0, 2 nt, 16 sc1)
+#endif
+// the same float4 as ldnt(ub + lane + 64 * j): `ub` is the wave-uniform row/tile base, the lane offset a voffset
+__device__ __forceinline__ f4 ldrow(const f4* ub, int lane, int j) {
+#if FA_RED_BUF
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<f4*>(ub), (short)0, 0x7fffffff,
+                                                                     0x00020000);
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, (lane + 64 * j) * 16, 0, FA_RED_AUX));
+#else
+  return ldnt(ub + lane + 64 * j);
+#endif
+}
+
 __device__ __forceinline__ float sgnf(float x) {  // torch.sign: -1, 0, +1 (NaN passes through)
   return x > 0.f ? 1.f : (x < 0.f ? -1.f : x);
 }
@@ -152,6 +169,11 @@ __device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int 
   const f4* __restrict__ xp = reinterpret_cast<const f4*>(r.x);
   const int sw = FULL ? V : r.sw;
   const int64_t c0 = r.col0 + (tile * FA_RED_WAVES + wave) * (64LL * sw) + lane;
+#if FA_RED_BUF
+  const f4* xu = xp + (int64_t)__builtin_amdgcn_readfirstlane((int)(c0 - lane));  // wave-uniform tile base
+#else
+  const f4* xu = xp + (c0 - lane);
+#endif
 
   bool ok[V];
 #pragma unroll
@@ -167,20 +189,20 @@ __device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int 
     const float w0 = W ? r.a[0] : 1.f;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      f4 t = ok[j] ? ldnt(xp + c0 + 64 * j) : f4{0.f, 0.f, 0.f, 0.f};
+      f4 t = ok[j] ? ldrow(xu, lane, j) : f4{0.f, 0.f, 0.f, 0.f};
       s[j] = W ? t * w0 : t;
     }
     k = 1;
   }
 
-  const f4* row = xp + (int64_t)k * r.ld4 + c0;
+  const f4* row = xu + (int64_t)k * r.ld4;  // client k's row at this wave's tile (lane offsets in ldrow)
   // U clients' loads, then their adds in arrival order
   auto load_group = [&](f4(&t)[U][V], const f4* rw) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < V; ++j)
-        t[u][j] = ok[j] ? ldnt(rw + u * r.ld4 + 64 * j) : f4{0.f, 0.f, 0.f, 0.f};
+        t[u][j] = ok[j] ? ldrow(rw + u * r.ld4, lane, j) : f4{0.f, 0.f, 0.f, 0.f};
   };
   auto add_group = [&](const f4(&t)[U][V], int k0) {
 #pragma unroll
@@ -219,7 +241,7 @@ __device__ __forceinline__ void reduce_tile(const RedArgs& r, int64_t tile, int 
     const float w = W ? r.a[k] : 1.f;
 #pragma unroll
     for (int j = 0; j < V; ++j) {
-      f4 t = ok[j] ? ldnt(row + 64 * j) : f4{0.f, 0.f, 0.f, 0.f};
+      f4 t = ok[j] ? ldrow(row, lane, j) : f4{0.f, 0.f, 0.f, 0.f};
       s[j] = W ? s[j] + w * t : s[j] + t;
     }
     row += r.ld4;
