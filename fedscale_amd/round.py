@@ -268,16 +268,19 @@ class DeviceRound:
         if self.policy == "fedbuff":
             a32, a64 = self._chunk_weights()
         acc_in = None if first else self.acc
-        if yogi is not None:
-            kx.reduce_yogi(x, n, L.P, a=a32, acc_in=acc_in, denom=denom32, out=out, **yogi)
-        elif mirror is not None:
-            kx.reduce_mirror(x, n, L.P, out, mirror, a=a32, acc_in=acc_in, denom=denom32)
-        else:
-            kx.reduce(x, n, L.P, out, a=a32, acc_in=acc_in, denom=denom32, finalize=True, host_ok=zc is not None)
         mode = 0 if self.policy == "fedavg" else 1
-        kx.side_accumulate(xi, n, L.Q, mode, w=a64, acc_i=self.acc_i, acc_d=self.acc_d, accumulate=not first)
-        if zc is not None:
-            st.release_host_rows()
+        try:
+            if yogi is not None:
+                kx.reduce_yogi(x, n, L.P, a=a32, acc_in=acc_in, denom=denom32, out=out, **yogi)
+            elif mirror is not None:
+                kx.reduce_mirror(x, n, L.P, out, mirror, a=a32, acc_in=acc_in, denom=denom32)
+            else:
+                kx.reduce(x, n, L.P, out, a=a32, acc_in=acc_in, denom=denom32, finalize=True,
+                          host_ok=zc is not None)
+            kx.side_accumulate(xi, n, L.Q, mode, w=a64, acc_i=self.acc_i, acc_d=self.acc_d, accumulate=not first)
+        finally:
+            if zc is not None:  # the mirror's rows are rewritten only after the stream has passed these reads
+                st.release_host_rows()
         kx.side_close(L.Q, mode, denom64, acc_i=self.acc_i, acc_d=self.acc_d, cur=cur_side, model=model_side)
 
     @on_stream
