@@ -54,6 +54,12 @@ yogi)
 head)
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/r3_head_prof -o run -- python3 bench.py --steps 10 --warmup 2 --cpu-seconds 0 --no-other-configs > $OUT/r3_head_prof.log 2>&1 || { tail -20 $OUT/r3_head_prof.log; exit 1; }
   grep '^{' $OUT/r3_head_prof.log | cut -c1-300 ;;
+headpmc)  # headline FETCH_SIZE / WRITE_SIZE passes (one counter block each), per-launch traffic into profiles/pmc_traffic.json
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 180 rocprofv3 --pmc $c --output-format csv -d $OUT/r3_head_$c -o run -- python3 bench.py --steps 3 --warmup 1 --cpu-seconds 0 --no-other-configs > $OUT/r3_head_$c.log 2>&1 || { tail -5 $OUT/r3_head_$c.log; exit 1; }
+  done
+  L=$(timeout -k 5 60 python -c "from fedscale_amd import kernels as kx; print(kx.reduce_launches(1000, 25000000))") || exit 1
+  python tools/pmc_parse.py $OUT/r3_head_FETCH_SIZE $OUT/r3_head_WRITE_SIZE fedavg_k1000_p25000000 $((4*1000*25000000 + 4*25000000)) k_reduce $L || exit 1 ;;
 dist)  # gloo rehearsals (ranks share the one GPU): per-rank kernel times on the N > 1 lines
   for n in 2 4; do
     timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 --master-port 2952$n bench.py --gpus $n --steps 5 --warmup 1 --dist-backend gloo --mem-fraction 0.15 --no-other-configs > $OUT/r3_dist$n.log 2>&1 || { tail -30 $OUT/r3_dist$n.log; exit 1; }
