@@ -397,15 +397,17 @@ class ClientStaging:
                  (self._hx_np[slot, e.offset:e.offset + e.numel] if e.kind == "f" else
                   self._hxi_np[slot, e.offset:e.offset + e.numel]).reshape(e.shape))
                 for e in self.layout.entries]
-        for (name, shape, dt, _), a in zip(views, values):
+        for a in values:
             if type(a) is not np.ndarray:
                 return False
+        self._claim_bulk(slot)
+        # validated entry by entry as it is copied: an error leaves the slot uncommitted (_bulk_hi is not
+        # advanced), so the next update written to it overwrites every entry
+        for (name, shape, dt, dst), a in zip(views, values):
             if a.shape != shape:
                 raise ValueError(f"{name}: shape {tuple(a.shape)} != model shape {shape}")
             if a.dtype != dt:
                 raise TypeError(f"{name}: dtype {a.dtype}, the model entry is {'float32' if dt == _F32 else 'int64'}")
-        self._claim_bulk(slot)
-        for (_, _, _, dst), a in zip(views, values):
             dst[...] = a
         self._bulk_hi = slot + 1
         return True
@@ -449,9 +451,10 @@ class ClientStaging:
 
     def release_host_rows(self):
         """After the launches that read ``host_rows()``: the mirror's rows are rewritten only once the stream
-        has passed them (the same event as an H2D out of the mirror)."""
-        with self._on():
-            self._bulk_ev.record(torch.cuda.current_stream(self._dev_index))
+        has passed them (the same event as an H2D out of the mirror).  The reads were issued on the dstream
+        (or, without one, on the current stream of this device)."""
+        self._bulk_ev.record(self.dstream.stream if self.dstream is not None
+                             else torch.cuda.current_stream(self._dev_index))
         self._bulk_busy = True
         self._bulk_lo = self._bulk_hi = 0
 
