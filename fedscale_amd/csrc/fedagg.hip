@@ -844,7 +844,7 @@ __device__ __forceinline__ void rows_load_lds(__amdgpu_buffer_rsrc_t r, uint32_t
 // the fused FedAvg chain (whose 64 extra live values otherwise go through AGPRs), so chain launches use it.
 template <bool WIDE, bool CHAIN, int GLDS, int QV>
 __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
-  static_assert(GLDS == 0 || GLDS == 1 || (GLDS == 2 && (QV == 16 || QV == 12)),
+  static_assert(GLDS == 0 || GLDS == 1 || (GLDS == 2 && (QV == 16 || QV == 12 || QV == 8)),
                 "GLDS: 0, 1 or 2 LDS slices per wave (2: 16 or 12 float4 per lane)");
   constexpr int NB = GLDS > 0 ? GLDS : 1;
   // ONE static LDS array, so it sits at LDS offset 0: the row slices first (the DMA addresses them from
@@ -986,8 +986,10 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
         else  // (GLDS - 1) x (alpha + 16 slice loads) may stay in flight
           if constexpr (QV == 16)
             asm volatile("s_waitcnt vmcnt(17)" ::: "memory");
-          else
+          else if constexpr (QV == 12)
             asm volatile("s_waitcnt vmcnt(13)" ::: "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
         f4 t[QV];
         const f4* src = myrow + (kk % NB) * (QV * 64);
 #pragma unroll
