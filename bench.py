@@ -399,7 +399,7 @@ class Workload:
             mine = losses[rank * K:(rank + 1) * K] if self.cmode else losses
             self.qf = dict(last=torch.empty(1, ld, device=dev), delta=torch.zeros(ld, device=dev),
                            sq=torch.zeros(self.Kg, dtype=torch.float64, device=dev),
-                           ws=kx.qfed_workspace(self.C, dev), hs=torch.zeros(2, device=dev), lr=lr,
+                           ws=kx.qfed_workspace(self.C, dev, ld, self.P), hs=torch.zeros(2, device=dev), lr=lr,
                            alpha=torch.tensor([np.float32(np.float_power(l + 1e-10, q)) for l in mine], device=dev),
                            c1=torch.tensor([np.float32(q * np.float_power(l + 1e-10, q - 1)) for l in losses],
                                            device=dev),

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, "libfedagg.so"))
-ABI_VERSION = 2  # fedagg.hip FA_ABI_VERSION
+ABI_VERSION = 3  # fedagg.hip FA_ABI_VERSION
 
 FA_ACCUMULATE = 1
 FA_FINALIZE = 2
@@ -44,9 +44,9 @@ SIGNATURES = {
     "fa_yogi_step": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32, _f32, _f32,
                             _f32, _i32, _c_void_p]),
     "fa_qfed_max_chunk": (_i32, []),
-    "fa_qfed_workspace_bytes": (_i64, [_i32]),
+    "fa_qfed_workspace_bytes": (_i64, [_i32, _i64, _i64]),
     "fa_qfed_accumulate": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p,
-                                  _c_void_p, _c_void_p, _i32, _c_void_p]),
+                                  _c_void_p, _c_void_p, _i64, _i32, _c_void_p]),
     "fa_qfed_hs": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _c_void_p]),
     "fa_qfed_finalize": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _c_void_p]),
     "fa_side_accumulate": (_i32, [_c_void_p, _i32, _i32, _i32, _i32, _c_void_p, _c_void_p, _c_void_p, _i32,

@@ -34,7 +34,8 @@
 
 // 2: fa_qfed_accumulate gained `chain`, fa_sgd_prox_step's dampening became double, and every launching
 //    entry point resolves its device from the stream / output pointer (fa_device.h)
-#define FA_ABI_VERSION 2
+// 3: fa_qfed_accumulate takes the workspace's size, fa_qfed_workspace_bytes the call's (ld, P) (deferred gathers)
+#define FA_ABI_VERSION 3
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
@@ -1299,15 +1300,65 @@ __global__ __launch_bounds__(256) void k_qfed_gather(const double* __restrict__ 
   sqnorm[k] += s;
 }
 
+// Deferred gathers (a call with several column windows and a workspace that holds every window's partials):
+// seg[w][y][k] = the y-th 16-row segment sum of window w's QF_GRID partial rows, all windows in one launch, then
+// per client, window by window in order: s = sum of the 16 segments from 0.0; sqnorm[k] += s — the same adds
+// in the same order as the per-window pair above, so the norms are bit-identical; one pair of launches per
+// call instead of one per window (each window's pair cost ~13 us: 2.5 % of config 5's 0.55 ms chain windows).
+__global__ __launch_bounds__(256) void k_qfed_gather_seg_win(const double* __restrict__ part, int nrows, int K,
+                                                             int64_t per_win, double* seg) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  const int rps = nrows / QF_GATHER_SEG;
+  const double* p = part + (int64_t)blockIdx.z * per_win + (int64_t)blockIdx.y * rps * K + k;
+  double s = 0.0;
+#pragma unroll 4
+  for (int r = 0; r < rps; ++r) s += p[(int64_t)r * K];
+  seg[((int64_t)blockIdx.z * QF_GATHER_SEG + blockIdx.y) * K + k] = s;
+}
+
+__global__ __launch_bounds__(256) void k_qfed_gather_win(const double* __restrict__ seg, int K, int nwin,
+                                                         double* sqnorm) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  double acc = sqnorm[k];
+  for (int w = 0; w < nwin; ++w) {
+    double s = 0.0;
+    for (int b = 0; b < QF_GATHER_SEG; ++b) s += seg[((int64_t)w * QF_GATHER_SEG + b) * K + k];
+    acc += s;
+  }
+  sqnorm[k] = acc;
+}
+
 extern "C" int fa_qfed_max_chunk(void) { return QF_MAXK; }
-extern "C" int64_t fa_qfed_workspace_bytes(int32_t K) {  // enough for either kernel family
-  const int64_t k = K > 0 ? K : 1;
+
+static int64_t qfed_window(int64_t ld, int64_t P, bool chain);
+// one window's partials + segments (the per-window gathers), either kernel family
+static int64_t qfed_ws_one(int64_t k) {
   const int64_t w1 = ((int64_t)QF_GRID + QF_GATHER_SEG) * k * 8, w2 = ((int64_t)QF2_ROWS + QF2_SEG) * k * 8;
   return w1 > w2 ? w1 : w2;
+}
+// every window's partials + segments (deferred gathers) of a call at (K, ld, P), chain or not
+static int64_t qfed_ws_deferred(int64_t k, int64_t ld, int64_t P, bool chain) {
+  const int64_t win = qfed_window(ld, P, chain), nwin = P > win ? (P + win - 1) / win : 1;
+  return nwin * ((int64_t)QF_GRID + QF_GATHER_SEG) * k * 8;
+}
+extern "C" int64_t fa_qfed_workspace_bytes(int32_t K, int64_t ld, int64_t P) {
+  const int64_t k = K > 0 ? K : 1;
+  int64_t b = qfed_ws_one(k);
+  if (ld >= P && P > 0) {
+    const int64_t c = qfed_ws_deferred(k, ld, P, true), n = qfed_ws_deferred(k, ld, P, false);
+    if (c > b) b = c;
+    if (n > b) b = n;
+  }
+  return b;
 }
 
 #ifndef QF_CHAIN_KERNEL
 #define QF_CHAIN_KERNEL 1
+#endif
+#ifndef QF_DEFER_GATHER
+#define QF_DEFER_GATHER 1  // one gather pair per call over every window's partials (workspace permitting)
 #endif
 #ifndef QF_CHAIN_GLDS
 #define QF_CHAIN_GLDS 1  // LDS-DMA slices per wave of the chain launches (profiles/r02_tune_qfed2.log)
@@ -1358,7 +1409,7 @@ extern "C" int64_t fa_qfed_launches(int64_t ld, int64_t P, int32_t chain) {
 
 static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const float* last, const float* alpha,
                         float lr, int fast, float* delta, float* chain, double* sqnorm, void* workspace,
-                        int32_t flags, hipStream_t st) {
+                        int64_t ws_bytes, int32_t flags, hipStream_t st) {
   QfArgs q{};
   q.x = x; q.ld4 = ld / 4; q.P4 = (P + 3) / 4; q.K = K; q.flags = flags; q.last = last; q.alpha = alpha;
   q.lr = lr; q.rlr = 1.0f / lr; q.delta = delta; q.chain = chain; q.part = (double*)workspace;
@@ -1368,8 +1419,14 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
   const bool wide = (int64_t)ld * 4 * QF_G <= QF_WIDE_BYTES;
   const int qv = chain ? QF_CHAIN_V : QF_V;
   const int64_t win = qfed_window(ld, P, chain != nullptr);
-  for (int64_t w0 = 0; w0 < P || w0 == 0; w0 += win) {
+  const int64_t nwin = P > win ? (P + win - 1) / win : 1;
+  const int64_t per_win = (int64_t)QF_GRID * K;  // doubles of one window's partial rows
+  // several windows and room for all their partials: one gather pair at the end (QF_DEFER_GATHER 0: off)
+  const bool defer = QF_DEFER_GATHER && nwin > 1 && ws_bytes >= qfed_ws_deferred(K, ld, P, chain != nullptr);
+  int64_t wi = 0;
+  for (int64_t w0 = 0; w0 < P || w0 == 0; w0 += win, ++wi) {
     QfArgs qw = q;
+    if (defer) qw.part = (double*)workspace + wi * per_win;
     const int64_t pw = P - w0 < win ? P - w0 : win;
     qw.x = x + w0; qw.last = last + w0; qw.delta = delta + w0; qw.chain = chain ? chain + w0 : nullptr;
     qw.P4 = (pw + 3) / 4;
@@ -1393,15 +1450,26 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
       hipLaunchKernelGGL((k_qfed_accum<false, false, QF_PLAIN_GLDS, QF_V>), dim3(QF_GRID), dim3(256), 0, st, qw);
     int e = check_launch("fa_qfed_accumulate");
     if (e) return e;
-    // the QF_GRID partial rows, summed in a fixed two-level order (16 segments of QF_GRID/16 rows)
-    double* seg = (double*)workspace + (int64_t)QF_GRID * K;
-    hipLaunchKernelGGL(k_qfed_gather_seg, dim3((K + 255) / 256, QF_GATHER_SEG), dim3(256), 0, st,
-                       (const double*)workspace, (int)QF_GRID, (int)K, seg);
-    hipLaunchKernelGGL(k_qfed_gather, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)seg,
-                       (int)QF_GATHER_SEG, (int)K, sqnorm);
-    e = check_launch("fa_qfed_accumulate(gather)");
-    if (e) return e;
+    if (!defer) {
+      // the QF_GRID partial rows, summed in a fixed two-level order (16 segments of QF_GRID/16 rows)
+      double* seg = (double*)workspace + per_win;
+      hipLaunchKernelGGL(k_qfed_gather_seg, dim3((K + 255) / 256, QF_GATHER_SEG), dim3(256), 0, st,
+                         (const double*)workspace, (int)QF_GRID, (int)K, seg);
+      hipLaunchKernelGGL(k_qfed_gather, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)seg,
+                         (int)QF_GATHER_SEG, (int)K, sqnorm);
+      e = check_launch("fa_qfed_accumulate(gather)");
+      if (e) return e;
+    }
     if (pw >= P - w0) break;
+  }
+  if (defer) {
+    const int64_t nw = wi + 1;  // windows launched
+    double* seg = (double*)workspace + nw * per_win;
+    hipLaunchKernelGGL(k_qfed_gather_seg_win, dim3((K + 255) / 256, QF_GATHER_SEG, (unsigned)nw), dim3(256), 0, st,
+                       (const double*)workspace, (int)QF_GRID, (int)K, per_win, seg);
+    hipLaunchKernelGGL(k_qfed_gather_win, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)seg, (int)K,
+                       (int)nw, sqnorm);
+    return check_launch("fa_qfed_accumulate(gather)");
   }
   return FA_OK;
 }
@@ -1444,11 +1512,14 @@ static int launch_qfed2(const float* x, int64_t ld, int32_t K, int64_t P, const 
 
 extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t P, const float* last,
                                   const float* alpha, float lr, float* delta, float* chain, double* sqnorm,
-                                  void* workspace, int32_t flags, fa_stream_t stream) {
+                                  void* workspace, int64_t workspace_bytes, int32_t flags, fa_stream_t stream) {
   if (K <= 0 || K > QF_MAXK) return fail(FA_E_RANGE, "fa_qfed_accumulate: K=%d outside [1, %d]", (int)K, QF_MAXK);
   if (P < 0 || ld < P || ld % 4) return fail(FA_E_ARG, "fa_qfed_accumulate: bad P/ld");
   if (!x || !last || !alpha || !delta || !sqnorm || !workspace)
     return fail(FA_E_ARG, "fa_qfed_accumulate: NULL pointer");
+  if (workspace_bytes < qfed_ws_one(K))
+    return fail(FA_E_ARG, "fa_qfed_accumulate: workspace of %lld bytes, needs >= %lld (fa_qfed_workspace_bytes)",
+                (long long)workspace_bytes, (long long)qfed_ws_one(K));
   if (!aligned16(x) || !aligned16(last) || !aligned16(delta) || !aligned16(chain))
     return fail(FA_E_ARG, "fa_qfed_accumulate: x/last/delta/chain must be 16-byte aligned");
   if (!(lr > 1e-30f && lr < 1e30f)) return fail(FA_E_ARG, "fa_qfed_accumulate: lr=%g outside (1e-30, 1e30)", (double)lr);
@@ -1457,7 +1528,8 @@ extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t
   const int fast = (lr >= 9.5367432e-07f && lr <= 1048576.f) ? 1 : 0;  // [2^-20, 2^20]
   const int kern = chain ? QF_CHAIN_KERNEL : QF_KERNEL;
   if (kern == 2) return launch_qfed2(x, ld, K, P, last, alpha, lr, fast, delta, chain, sqnorm, workspace, flags, st);
-  return launch_qfed1(x, ld, K, P, last, alpha, lr, fast, delta, chain, sqnorm, workspace, flags, st);
+  return launch_qfed1(x, ld, K, P, last, alpha, lr, fast, delta, chain, sqnorm, workspace, workspace_bytes, flags,
+                      st);
 }
 
 // hs (optimizers.py:96-98) is a sequential fp32 sum in arrival order, so its final add chain stays on one

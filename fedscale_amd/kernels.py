@@ -142,8 +142,10 @@ def reduce_launches(K: int, P: int, weighted: bool = False) -> int:
     return int(N.load().fa_reduce_launches(int(K), int(P), 1 if weighted else 0))
 
 
-def qfed_workspace(K: int, device) -> torch.Tensor:
-    nbytes = N.load().fa_qfed_workspace_bytes(K)
+def qfed_workspace(K: int, device, ld: int = 0, P: int = 0) -> torch.Tensor:
+    """Workspace of fa_qfed_accumulate for chunks of <= K clients; with the rows' (ld, P) it holds every column
+    window's partial norms, so each call gathers them once instead of after every window (same bits)."""
+    nbytes = N.load().fa_qfed_workspace_bytes(K, int(ld), int(P))
     return torch.empty((nbytes + 7) // 8, dtype=torch.float64, device=device)
 
 
@@ -158,10 +160,10 @@ def qfed_accumulate(x, K, P, *, last, alpha, lr, delta, sqnorm, workspace, accum
     _dev(alpha, torch.float32, "alpha", K, align=4)
     _dev(sqnorm, torch.float64, "sqnorm", K, align=8)
     _dev(workspace, torch.float64, "workspace")
-    if workspace.numel() * 8 < N.load().fa_qfed_workspace_bytes(K):
+    if workspace.numel() * 8 < N.load().fa_qfed_workspace_bytes(K, 0, 0):
         raise ValueError("workspace too small")
     call("fa_qfed_accumulate", ptr(x), ld, K, P, ptr(last), ptr(alpha), float(lr), ptr(delta), ptr(chain),
-         ptr(sqnorm), ptr(workspace), FA_ACCUMULATE if accumulate else 0, _stream(delta))
+         ptr(sqnorm), ptr(workspace), workspace.numel() * 8, FA_ACCUMULATE if accumulate else 0, _stream(delta))
 
 
 def qfed_hs(sqnorm, c1, c2, K, hs_out):

@@ -137,7 +137,7 @@ class DeviceRound:
         self.delta_s = torch.zeros(L.ldq, dtype=torch.float32, device=dev)
         self.sqnorm = torch.zeros(self.K, dtype=torch.float64, device=dev)       # fp32 bucket part (per shard)
         self.sqnorm_side = torch.zeros(self.K, dtype=torch.float64, device=dev)  # side table part (replicated)
-        self.workspace = kx.qfed_workspace(self.cap, dev)
+        self.workspace = kx.qfed_workspace(self.cap, dev, L.ld, L.P)
         self.alpha = np.zeros(self.K, dtype=np.float32)
         self.c1 = np.zeros(self.K, dtype=np.float32)
         self.c2 = np.zeros(self.K, dtype=np.float32)

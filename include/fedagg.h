@@ -9,7 +9,8 @@
  * Conventions (all entry points):
  *   - return 0 on success, a negative FA_E* code on failure; fa_last_error_string() describes the
  *     last failure of the calling thread.  No exception crosses the ABI.
- *   - every pointer is DEVICE memory owned by the caller (16-byte aligned); every launch is
+ *   - every pointer is DEVICE memory owned by the caller (16-byte aligned), except where an entry point
+ *     says it may be pinned host memory (fa_reduce_mirror, fa_side_accumulate's xi); every launch is
  *     asynchronous on the caller's `stream` (a hipStream_t) with no implicit synchronisation.
  *     Functions are stateless and reentrant.
  *   - the device: a call's work runs on the GPU that holds its output.  A non-NULL `stream` must be a
@@ -109,7 +110,7 @@ int fa_yogi_step(const float* cur, const float* last, float* m, float* v, float*
 /*
  * Number of k_qfed_accum launches one fa_qfed_accumulate call makes for rows of ld floats and P columns,
  * with (chain != 0) or without the fused FedAvg chain: long rows run as column windows of one round of tiles
- * (4,194,304 columns; 3,145,728 for chain launches, whose tiles are 12 float4 per lane wide).  For reporting
+ * (4,194,304 columns; 2,097,152 for chain launches, whose tiles are 8 float4 per lane wide).  For reporting
  * per-launch figures (bench.py); no reference counterpart.
  */
 int64_t fa_qfed_launches(int64_t ld, int64_t P, int32_t chain);
@@ -124,13 +125,16 @@ int64_t fa_qfed_launches(int64_t ld, int64_t P, int32_t chain);
  * and, through `chain`, the FedAvg sum the reference computes on the same inputs (aggregator.py:497-503,
  * its model_weights): fa_reduce(chain, ld, 1, P, ..., FA_FINALIZE, denom = K) then gives the mean.
  * alpha: device fp32[K] = fp32(float_power(loss_k + 1e-10, q)).  sqnorm: device fp64[K].
- * workspace: device memory of fa_qfed_workspace_bytes(K) bytes.
+ * workspace: device memory of `workspace_bytes` bytes, at least fa_qfed_workspace_bytes(K, 0, 0) (one column
+ * window's per-workgroup partial norms: the gathers then run after every window).  fa_qfed_workspace_bytes(K, ld,
+ * P) holds every window's partials of a call at (ld, P), chain or not: the gathers then run once per call
+ * (ABI 3; the per-window form cost ~13 us a window).  Either way the norms are the same bits.
  */
 int fa_qfed_max_chunk(void);
-int64_t fa_qfed_workspace_bytes(int32_t K);
+int64_t fa_qfed_workspace_bytes(int32_t K, int64_t ld, int64_t P);
 int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t P, const float* last, const float* alpha,
-                       float lr, float* delta, float* chain, double* sqnorm, void* workspace, int32_t flags,
-                       fa_stream_t stream);
+                       float lr, float* delta, float* chain, double* sqnorm, void* workspace, int64_t workspace_bytes,
+                       int32_t flags, fa_stream_t stream);
 
 /*
  * q-FedAvg Lipschitz estimate, the fp32 recurrence of optimizers.py:96-98 in arrival order:

@@ -119,6 +119,63 @@ def test_qfed_accumulate_wide_rows_and_column_windows(gpu_device, K, P):
     np.testing.assert_allclose(sq.cpu().numpy(), np.array(want_sq), rtol=1e-9)
 
 
+@pytest.mark.parametrize("chain", [False, True], ids=["plain", "chain"])
+@pytest.mark.parametrize("K,P", [(37, 9_000_001), (5, 4_194_305), (3, 35_000_000)])
+def test_qfed_deferred_gathers_same_bits(gpu_device, K, P, chain):
+    """One call over several column windows gathers every window's partial norms once, at the end (the workspace
+    of fa_qfed_workspace_bytes(K, ld, P) holds them all); the same windows as separate one-window calls gather
+    after each.  Both add the same fp64 terms in the same order: norms, delta and chain are bit-identical, over
+    a first and a FA_ACCUMULATE call.  (3 x 35 M: more windows than a one-window workspace holds, so the
+    wrapper's workspace of fa_qfed_workspace_bytes(K) alone would gather per window: both sizes are run.)"""
+    from fedscale_amd import _native
+    from fedscale_amd import kernels as kx
+    from fedscale_amd import synth
+    from fedscale_amd._native import FA_ACCUMULATE
+    from fedscale_amd.bucket import round_up
+    from fedscale_amd.state import raw_stream
+
+    ld = round_up(P, 64)
+    n = kx.qfed_launches(ld, P, chain)
+    win = 256 * 4 * (8 if chain else 16) * 256  # fedagg.hip qfed_window: one round of full-width tiles
+    assert n == -(-P // win) and n > 1
+    x = torch.empty(K, ld, device="cuda")
+    synth.fill(x, K, P, seed=21)
+    last = torch.empty(1, ld, device="cuda")
+    synth.fill(last, 1, P, seed=21 + 90000, scale_noise=0.0)
+    last = last[0]
+    alpha = torch.rand(K, device="cuda") + 0.5
+    st = raw_stream(0)
+
+    def state():
+        return (torch.zeros(ld, device="cuda"), torch.zeros(ld, device="cuda") if chain else None,
+                torch.zeros(K, dtype=torch.float64, device="cuda"))
+
+    runs = {}
+    for name, ws in (("one_call_deferred", kx.qfed_workspace(K, "cuda", ld, P)),
+                     ("one_call_small_ws", kx.qfed_workspace(K, "cuda"))):
+        delta, ch, sq = state()
+        for acc in (False, True):
+            kx.qfed_accumulate(x, K, P, last=last, alpha=alpha, lr=0.05, delta=delta, sqnorm=sq, workspace=ws,
+                               accumulate=acc, chain=ch)
+        runs[name] = (delta, ch, sq)
+    # the per-window reference: one call per window (a single window always gathers right after it)
+    ws = kx.qfed_workspace(K, "cuda")
+    delta, ch, sq = state()
+    for acc in (False, True):
+        for w0 in range(0, P, win):
+            pw = min(win, P - w0)
+            _native.call("fa_qfed_accumulate", x.data_ptr() + 4 * w0, ld, K, pw, last.data_ptr() + 4 * w0,
+                         alpha.data_ptr(), 0.05, delta.data_ptr() + 4 * w0,
+                         ch.data_ptr() + 4 * w0 if chain else None, sq.data_ptr(), ws.data_ptr(), ws.numel() * 8,
+                         FA_ACCUMULATE if acc else 0, st)
+    torch.cuda.synchronize()
+    for name, (d1, c1, s1) in runs.items():
+        assert torch.equal(s1, sq), f"{name}: squared norms differ from the per-window gathers"
+        assert torch.equal(d1, delta), name
+        if chain:
+            assert torch.equal(c1, ch), name
+
+
 @pytest.mark.parametrize("name", ["fedavg_wide_k64", "fedbuff_k8", "qfedavg_q1"])
 def test_async_ingress_staging_matches_reference(gpu_device, name):
     """ClientStaging(async_ingress=True): the gather + H2D of each update runs on a background thread in

@@ -28,12 +28,12 @@ def main():
         lib = ctypes.CDLL(path)
         f = lib.fa_qfed_accumulate
         f.restype = I32
-        f.argtypes = [V, I64, I32, I64, V, V, F, V, V, V, V, I32, V]
+        f.argtypes = [V, I64, I32, I64, V, V, F, V, V, V, V, I64, I32, V]
         ws = lib.fa_qfed_workspace_bytes
-        ws.restype, ws.argtypes = I64, [I32]
+        ws.restype, ws.argtypes = I64, [I32, I64, I64]
         name = os.path.basename(path)[len("libfedagg_qf2_"):-3]
         for chain in (False, True):
-            libs[name + ("+chain" if chain else "")] = (f, chain, ws(K))
+            libs[name + ("+chain" if chain else "")] = (f, chain, ws(K, round_up(P, 64), P))
     ld = round_up(P, 64)
     x = torch.empty(K, ld, device="cuda")
     synth.fill(x, K, P, seed=3)
@@ -49,14 +49,14 @@ def main():
     rels = {}
     ref = ref_chain = ref_sq = None
     for r in range(rounds):
-        for n, (f, use_chain, _) in libs.items():
+        for n, (f, use_chain, wsb) in libs.items():
             sq.zero_()
             args = (x.data_ptr(), ld, K, P, last.data_ptr(), alpha.data_ptr(), 0.05, delta.data_ptr(),
-                    chain.data_ptr() if use_chain else None, sq.data_ptr(), ws.data_ptr(), 0, st)
+                    chain.data_ptr() if use_chain else None, sq.data_ptr(), ws.data_ptr(), wsb, 0, st)
             assert f(*args) == 0, n
             torch.cuda.synchronize()
             if later:  # time later passes: the chains continue from the first call's delta / chain
-                args = args[:11] + (1,) + args[12:]
+                args = args[:12] + (1,) + args[13:]
             if ref is None:
                 ref, ref_sq = delta.clone(), sq.clone()
             else:
