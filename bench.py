@@ -661,6 +661,11 @@ def main():
     local_dev = local if args.dist_backend == "nccl" else local % max(1, ndev)
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
+    # as the drop-in's init_model does (DeviceAggregatorMixin.device_numa_bind): the thread that stages uploads
+    # in pinned memory runs on the GPU's NUMA node (fedscale_amd/hostnuma.py)
+    from fedscale_amd.hostnuma import bind_to_gpu
+
+    numa_node = bind_to_gpu(dev)
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -766,6 +771,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic full-weight client updates (base + noise, hash-generated on device), HBM-resident",
+            "host_numa_node": numa_node,
             "config": config,
             "hbm_gbps": achieved,
             "kernel_ms": kern_ms_max,

@@ -75,6 +75,9 @@ class DeviceAggregatorMixin:
     device_egress_past_versions = 8
     #: GPU ordinals to shard the model over inside this process (None: FEDAGG_DEVICES, else one GPU)
     device_shards = None
+    #: bind the main thread (which stages every upload into pinned memory) to the CPUs of the GPU's NUMA node,
+    #: so the staging lands next to the GPU's PCIe link (fedscale_amd/hostnuma.py); single-GPU adapters only
+    device_numa_bind = True
 
     _device_round = None
 
@@ -123,6 +126,10 @@ class DeviceAggregatorMixin:
             dev = devs[0] if devs else self._aggregation_device()
             opt = TorchServerOptimizer(self.args.gradient_policy, self.args, dev)
             self.model_wrapper = TorchModelAdapter(model, optimizer=opt, device=dev)
+            if self.device_numa_bind:
+                from ...hostnuma import bind_to_gpu
+
+                bind_to_gpu(getattr(self.model_wrapper, "device", dev))
 
     def _wrapper(self) -> TorchModelAdapter:
         w = self.model_wrapper
