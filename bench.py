@@ -237,7 +237,7 @@ def c1_job_conf() -> dict:
         return json.load(f)
 
 
-def c1_host_round(dev, seed: int, rounds: int = 50) -> dict:
+def c1_host_round(dev, seed: int, rounds: int = 300) -> dict:
     """BASELINE config 1 (FEMNIST small-CNN, K = num_participants of the job config = 10) through the drop-in:
     start_round, K on_result calls with host dicts (pinned staging + H2D), the fused reduce, and get_weights()
     (D2H) — the whole round the reference runs on the CPU (aggregator.py:489-511, torch_model_adapter.py:23-47)."""
@@ -278,7 +278,7 @@ def c1_host_round(dev, seed: int, rounds: int = 50) -> dict:
             "note": "host dicts in, global model out (get_weights); median of %d rounds" % rounds}
 
 
-def cpu_baseline_c1(seed: int, rounds: int = 50) -> dict:
+def cpu_baseline_c1(seed: int, rounds: int = 300) -> dict:
     """The oracle's restatement of the same config-1 round on one host core (cpu_baseline leg)."""
     import numpy as np
 
