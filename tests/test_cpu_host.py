@@ -179,3 +179,22 @@ def test_native_host_gather_streaming_copy_odd_offsets(workers):
         want[o:o + n] = src_buf[s_at:s_at + n]
         s_at += n + 5
     np.testing.assert_array_equal(dst, want)
+
+
+def test_qfed_workspace_sizes():
+    """fa_qfed_workspace_bytes (host-only): the one-window size for (K, 0, 0); for a call's (ld, P) room for every
+    column window's partial norms of either launch form (chain windows are 2,097,152 columns, plain 4,194,304),
+    so fa_qfed_accumulate gathers once per call; fa_qfed_accumulate refuses a workspace below the one-window size."""
+    from fedscale_amd._native import FA_ACCUMULATE, FedAggError, call, load
+
+    lib = load()
+    for K in (1, 37, 462, 1024):
+        one = lib.fa_qfed_workspace_bytes(K, 0, 0)
+        assert one >= (256 + 16) * K * 8
+        for P in (1_000_000, 25_000_000, 100_000_000):
+            ld = -(-P // 64) * 64
+            nwin = -(-P // 2_097_152)
+            b = lib.fa_qfed_workspace_bytes(K, ld, P)
+            assert b >= one and b >= nwin * (256 + 16) * K * 8, (K, P, b)
+    with pytest.raises(FedAggError, match="workspace"):
+        call("fa_qfed_accumulate", 16, 64, 4, 64, 16, 16, 0.05, 16, None, 16, 16, 8, FA_ACCUMULATE, None)
