@@ -278,6 +278,53 @@ def c1_host_round(dev, seed: int, rounds: int = 300) -> dict:
             "note": "host dicts in, global model out (get_weights); median of %d rounds" % rounds}
 
 
+def pcie_inclusive_leg(dev, seed: int, K: int = 64, rounds: int = 2) -> dict:
+    """SURVEY §8d's second figure: the headline model's round as a deployment sees it, from the executors'
+    pickled upload payloads (CLIENT_EXECUTE_COMPLETION) through the mixin's zero-copy deserialize_response
+    (aggregator.py:704), the pinned gather + H2D and the reduce, to get_weights() (D2H egress,
+    torch_model_adapter.py:41-47).  25 M fp32 as 10 tensors of 2.5 M (100 MB per update); 8 distinct payloads
+    reused.  Never `value`: it is bound by one PCIe link (PCIe-inclusive rate)."""
+    import pickle
+
+    import numpy as np
+    import torch
+
+    from fedscale_amd import synth
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    names, shapes = [f"l{i}.weight" for i in range(10)], [(2500, 1000)] * 10
+    model = synth.LayoutModule(names, shapes, [torch.float32] * 10)
+    adapter = TorchModelAdapter(model, device=dev)
+    agg = DeviceAggregator(adapter)
+    rng = np.random.default_rng(seed)
+    payloads = []
+    for i in range(8):
+        up = {n: t.numpy() + rng.standard_normal(t.shape, dtype=np.float32) * np.float32(0.01)
+              for n, t in model.state_dict().items()}
+        payloads.append(pickle.dumps({"client_id": i, "moving_loss": 1.0, "trained_size": 200, "success": True,
+                                      "utility": 1.0, "update_weight": up, "wall_duration": 0}))
+        del up
+    ts = []
+    for r in range(rounds + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        agg.start_round(K)
+        for k in range(K):
+            agg.on_result(agg.deserialize_response(payloads[k % 8]))
+        adapter.get_weights()
+        if r:
+            ts.append(time.perf_counter() - t0)
+    s = float(np.median(ts))
+    P = adapter.layout.P_full
+    del agg, adapter, payloads
+    torch.cuda.empty_cache()
+    return {"clients": K, "params": P, "round_ms": s * 1e3, "client_updates_per_s": K / s,
+            "host_to_device_GBps": 4 * K * P / s / 1e9,
+            "note": "from pickled executor payloads: zero-copy deserialize_response, pinned gather + H2D, reduce, "
+                    "get_weights() D2H; median of %d rounds; bound by one PCIe link, never `value`" % rounds}
+
+
 def cpu_baseline_c1(seed: int, rounds: int = 300) -> dict:
     """The oracle's restatement of the same config-1 round on one host core (cpu_baseline leg)."""
     import numpy as np
@@ -608,6 +655,7 @@ def single_gpu_configs(dev, seed, shards, backend, cpu_budget) -> dict:
         "c4s", dict(CONFIGS["c4"], params=25_000_000 // 4), dev, 0, 1, shards, seed, backend, steps=10)
     out["c5_qfedavg_shard_of_8"] = config_line(
         "c5s", dict(CONFIGS["c5"], params=100_000_000 // 8), dev, 0, 1, shards, seed, backend, steps=3, warmup=1)
+    out["headline_model_pcie_inclusive"] = pcie_inclusive_leg(dev, seed)
     if cpu_budget > 0:
         out["c1_femnist_cnn_k10_host_round"]["cpu_baseline"] = cpu_baseline_c1(seed)
         for key, name, share in (("c2_synthetic_k100_p1M", "c2", 0.1), ("c3_resnet18_layout_k1000_p11191242", "c3", 0.4),
