@@ -34,6 +34,7 @@ _c_void_p, _i32, _i64, _f32, _f64, _u32 = (ctypes.c_void_p, ctypes.c_int32, ctyp
 SIGNATURES = {
     "fa_abi_version": (_i32, []),
     "fa_last_error_string": (ctypes.c_char_p, []),
+    "fa_pointer_kind": (_i32, [_c_void_p]),
     "fa_reduce": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _f32, _i32, _c_void_p]),
     "fa_reduce_mirror": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32, _i32,
                                 _c_void_p]),

@@ -38,6 +38,23 @@ inline int fa_pointer_device(const void* p) {
   return at.type == hipMemoryTypeDevice ? at.device : -1;
 }
 
+// 1: host memory the GPU dereferences at the same address (pinned and mapped, e.g. hipHostMalloc / torch
+// pin_memory); 0: device memory; -1: anything else (pageable, unregistered, managed, or mapped at another
+// address) — a kernel must never be handed such a pointer (it would fault the GPU).  NULL: 0.
+inline int fa_host_mapped(const void* p) {
+  if (!p) return 0;
+  hipPointerAttribute_t at;
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  if (at.type == hipMemoryTypeDevice) return 0;
+  // the same mapping on both sides (compared with each other, so it holds whether the runtime reports the
+  // allocation's base or the queried address)
+  if (at.type == hipMemoryTypeHost && at.hostPointer && at.devicePointer == at.hostPointer) return 1;
+  return -1;
+}
+
 class DevScope {
  public:
   DevScope(const char* what, fa_stream_t stream, const void* anchor) : saved_(fa_t_dev) {

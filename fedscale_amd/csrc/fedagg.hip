@@ -65,6 +65,7 @@ extern "C" __attribute__((visibility("hidden"))) int fa_internal_set_error(int c
 }
 
 extern "C" int fa_abi_version(void) { return FA_ABI_VERSION; }
+extern "C" int fa_pointer_kind(const void* p) { return fa_host_mapped(p); }
 extern "C" const char* fa_last_error_string(void) { return g_err; }
 
 // ------------------------------------------------------------------------------------------------
@@ -624,6 +625,8 @@ extern "C" int fa_reduce(const float* x, int64_t ld, int32_t K, int64_t P, const
   int e = check_reduce_args("fa_reduce", x, ld, K, P, acc_in, out, flags);
   if (e) return e;
   if (P == 0) return FA_OK;
+  if (K > 0 && fa_host_mapped(x) < 0)
+    return fail(FA_E_ARG, "fa_reduce: x must be device memory or pinned host memory mapped for the GPU");
   RedArgs r{};
   r.x = x; r.ld4 = ld / 4; r.P4 = (P + 3) / 4; r.K = K; r.flags = flags; r.a = a; r.acc_in = acc_in;
   r.out = out; r.denom = denom;
@@ -641,6 +644,9 @@ extern "C" int fa_reduce_mirror(const float* x, int64_t ld, int32_t K, int64_t P
   if (!(flags & FA_FINALIZE)) return fail(FA_E_ARG, "fa_reduce_mirror: needs FA_FINALIZE");
   if (!mirror || !aligned16(mirror)) return fail(FA_E_ARG, "fa_reduce_mirror: mirror NULL or not 16-byte aligned");
   if (P == 0) return FA_OK;
+  if (fa_host_mapped(x) < 0 || fa_host_mapped(mirror) < 0)
+    return fail(FA_E_ARG, "fa_reduce_mirror: x and mirror must be device memory or pinned host memory mapped for "
+                          "the GPU (pageable memory would fault it)");
   RedArgs r{};
   r.x = x; r.ld4 = ld / 4; r.P4 = (P + 3) / 4; r.K = K; r.flags = flags; r.a = a; r.acc_in = acc_in;
   r.out = out; r.denom = denom; r.mean_out = mirror;
@@ -1648,6 +1654,8 @@ extern "C" int fa_side_accumulate(const int64_t* xi, int32_t ldq, int32_t K, int
   if (mode == 1 && (!acc_d || !w)) return fail(FA_E_ARG, "fa_side_accumulate: acc_d/w NULL");
   if (mode != 0 && mode != 1) return fail(FA_E_ARG, "fa_side_accumulate: mode %d", (int)mode);
   if (K == 0) return FA_OK;
+  if (fa_host_mapped(xi) < 0)
+    return fail(FA_E_ARG, "fa_side_accumulate: xi must be device memory or pinned host memory mapped for the GPU");
   FA_DEVICE_SCOPE("fa_side_accumulate", stream, mode == 0 ? (const void*)acc_i : (const void*)acc_d);
   hipLaunchKernelGGL(k_side_accum, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, xi, ldq, K, Q, mode, w,
                      acc_i, acc_d, (flags & FA_ACCUMULATE) ? 1 : 0);

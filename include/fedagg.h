@@ -54,6 +54,12 @@ enum {
 int fa_abi_version(void);
 const char* fa_last_error_string(void);
 
+/* What a pointer is to the GPU: 0 device memory (or NULL), 1 pinned host memory the GPU reads at the same
+ * address (hipHostMalloc, torch pin_memory), -1 anything else (pageable, unregistered, managed) — no entry point
+ * hands such a pointer to a kernel: fa_reduce, fa_reduce_mirror and fa_side_accumulate reject it with FA_E_ARG.
+ * No reference counterpart (the host-memory operands of the zero-copy round). */
+int fa_pointer_kind(const void* p);
+
 /*
  * Weighted in-order K-way column reduction over one chunk of K client updates.
  *   chain_p = FA_ACCUMULATE ? acc_in[p] : w_0*x[0][p]      (w_k = a[k], or 1 when a == NULL)

@@ -190,3 +190,20 @@ def test_chunked_small_round_keeps_the_h2d_path(gpu_device, monkeypatch):
     mir = [c for c in calls if c[0] == "fa_reduce_mirror"]
     assert len(mir) == 1 and mir[0][1][0] == adapter.staging.x.data_ptr()
     assert_state_equal(adapter.get_weights(), _oracle_round(ups), "chunked")
+
+
+def test_pointer_kinds_and_pageable_rejection(gpu_device):
+    """fa_pointer_kind tells device, pinned-and-mapped and other host memory apart without launching anything;
+    the entry points that may read host memory check it first (pageable memory would fault the GPU)."""
+    from fedscale_amd import _native
+
+    lib = _native.load()
+    dev = torch.zeros(64, device=gpu_device)
+    pinned = torch.zeros(64).pin_memory()
+    pageable = np.zeros(64, dtype=np.float32)
+    assert lib.fa_pointer_kind(dev.data_ptr()) == 0
+    assert lib.fa_pointer_kind(None) == 0
+    assert lib.fa_pointer_kind(pinned.data_ptr()) == 1
+    assert lib.fa_pointer_kind(pinned.data_ptr() + 64) == 1  # inside the allocation
+    assert lib.fa_pointer_kind(pageable.ctypes.data) == -1
+    assert lib.fa_pointer_kind(torch.zeros(64).data_ptr()) == -1
