@@ -667,7 +667,7 @@ def single_gpu_configs(dev, seed, shards, backend, cpu_budget) -> dict:
     return out
 
 
-def run_selfcheck(world: int, timeout_s: int = 240) -> dict:
+def run_selfcheck(world: int, timeout_s: int = 150) -> dict:
     """fedscale_amd.selfcheck over GPUs 0..N-1 in a child process (rank 0, N > 1): the sharded drop-in against
     one GPU, bit for bit, with every launch checked against its part's stream.  Summarised for the JSON line."""
     import subprocess
