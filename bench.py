@@ -278,7 +278,7 @@ def c1_host_round(dev, seed: int, rounds: int = 300) -> dict:
             "note": "host dicts in, global model out (get_weights); median of %d rounds" % rounds}
 
 
-def pcie_inclusive_leg(dev, seed: int, K: int = 64, rounds: int = 2) -> dict:
+def pcie_inclusive_leg(dev, seed: int, K: int = 64, rounds: int = 6) -> dict:
     """SURVEY §8d's second figure: the headline model's round as a deployment sees it, from the executors'
     pickled upload payloads (CLIENT_EXECUTE_COMPLETION) through the mixin's zero-copy deserialize_response
     (aggregator.py:704), the pinned gather + H2D and the reduce, to get_weights() (D2H egress,
@@ -315,14 +315,16 @@ def pcie_inclusive_leg(dev, seed: int, K: int = 64, rounds: int = 2) -> dict:
         adapter.get_weights()
         if r:
             ts.append(time.perf_counter() - t0)
-    s = float(np.median(ts))
+    s, smin = float(np.median(ts)), float(np.min(ts))
     P = adapter.layout.P_full
     del agg, adapter, payloads
     torch.cuda.empty_cache()
-    return {"clients": K, "params": P, "round_ms": s * 1e3, "client_updates_per_s": K / s,
-            "host_to_device_GBps": 4 * K * P / s / 1e9,
+    return {"clients": K, "params": P, "round_ms": s * 1e3, "round_ms_min": smin * 1e3,
+            "rounds_ms": [t * 1e3 for t in ts], "client_updates_per_s": K / s, "client_updates_per_s_best": K / smin,
+            "host_to_device_GBps": 4 * K * P / s / 1e9, "host_to_device_GBps_best": 4 * K * P / smin / 1e9,
             "note": "from pickled executor payloads: zero-copy deserialize_response, pinned gather + H2D, reduce, "
-                    "get_weights() D2H; median of %d rounds; bound by one PCIe link, never `value`" % rounds}
+                    "get_weights() D2H; median and min of %d rounds after one warm-up round; bound by one PCIe "
+                    "link, never `value`" % rounds}
 
 
 def cpu_baseline_c1(seed: int, rounds: int = 300) -> dict:
@@ -505,6 +507,8 @@ class Workload:
                 kx.reduce(x, n, P, self.out, a=a, acc_in=acc_in, denom=self.denom, finalize=True)
             else:  # as the drop-in runs FedYoGi: the mean, then the YoGi step over it (TorchModelAdapter)
                 kx.reduce(x, n, P, self.mean, a=a, acc_in=acc_in, denom=self.denom, finalize=True)
+                if ev is not None and len(ev) > 2:  # between the two kernels: each one's time on its own
+                    ev[2].record(st)
                 y = self.yogi
                 kx.yogi_step(self.mean, y["last"], y["m"], y["v"], self.out, P, init=y["init"],
                              **{k: y[k] for k in ("eta", "tau", "beta", "omb", "omb2")})
@@ -574,14 +578,19 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend):
 
     for _ in range(warmup):
         w.step()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    split = w.yogi is not None and not w.cmode  # FedYoGi: a third event between the mean and the YoGi step
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3 if split else 2)) for _ in range(steps)]
     _sync_all(dev, world)
     t0 = time.perf_counter()
     for i in range(steps):
         w.step(evs[i])
     _sync_all(dev, world)
     wall = time.perf_counter() - t0
-    kern_ms = float(np.mean([s.elapsed_time(e) for s, e in evs]))
+    kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    w.split_ms = None
+    if split:  # (mean of k_reduce's launches, mean of k_yogi_step) per step, max over ranks
+        w.split_ms = _max_over_ranks([float(np.mean([e[0].elapsed_time(e[2]) for e in evs])),
+                                      float(np.mean([e[2].elapsed_time(e[1]) for e in evs]))], dev, world, backend)
     return _max_over_ranks([wall, kern_ms], dev, world, backend), kern_ms, _all_ranks(kern_ms, dev, world, backend)
 
 
@@ -599,6 +608,20 @@ def config_line(name, cfg, dev, rank, world, shards, seed, backend, steps=5, war
            "client_updates_per_s": cfg["clients"] / (ms * 1e-3),
            "hbm_gbps_per_gpu": w.alg_bytes / (ms * 1e-3) / 1e9, "dominant_kernel_ms": kern_max,
            "hbm_gbps_kernel": w.alg_bytes / (kern_max * 1e-3) / 1e9}
+    if getattr(w, "split_ms", None):
+        from fedscale_amd import kernels as kx
+
+        red_ms, yogi_ms = w.split_ms
+        K_, P_ = w.K, w.P
+        out["kernels"] = {
+            "k_reduce (fa_reduce FA_FINALIZE, the mean)": {
+                "ms": red_ms, "launches": len(w.passes) * kx.reduce_launches(w.C if len(w.passes) > 1 else K_, P_),
+                "alg_bytes": 4 * K_ * P_ + 4 * P_, "hbm_gbps": (4 * K_ * P_ + 4 * P_) / (red_ms * 1e-3) / 1e9},
+            "k_yogi_step (fa_yogi_step)": {
+                "ms": yogi_ms, "launches": 1, "alg_bytes": 28 * P_, "hbm_gbps": 28 * P_ / (yogi_ms * 1e-3) / 1e9,
+                "note": "reads mean, last, m, v; writes m, v, new (16P + 12P)"},
+            "note": "one HIP event pair per kernel, on the launch stream; rocprofv3 of the same round: "
+                    "profiles/r04_c4_fedyogi_unfused_kernel_stats.csv"}
     if cfg["policy"] == "qfedavg":
         out["mean_chain"] = w.mean_chain
         if w.mean_chain:
@@ -696,6 +719,55 @@ def run_selfcheck(world: int, timeout_s: int = 150) -> dict:
     return out
 
 
+def run_inproc_bench(world: int, K: int, P: int, backend: str, timeout_s: int = 240) -> dict:
+    """fedscale_amd.inproc_bench in a child process (rank 0, N > 1): a timed device-resident round of the
+    in-process drop-in (ShardedModelAdapter over GPUs 0..N-1, the way FedScale's single-process aggregator is
+    deployed on a node) beside the single-device adapter.  With fewer GPUs than ranks (a gloo rehearsal on one
+    card) the parts share the visible GPUs (copy transport): plumbing only."""
+    import subprocess
+
+    import torch
+
+    nd = torch.cuda.device_count()
+    devs = [i % max(1, nd) for i in range(world)]
+    cmd = [sys.executable, "-m", "fedscale_amd.inproc_bench", "--devices", ",".join(map(str, devs)),
+           "--clients", str(K), "--params", str(P)]
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"devices": devs, "ok": False, "error": f"no result within {timeout_s} s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if not lines:
+        return {"devices": devs, "ok": False, "rc": r.returncode, "error": r.stderr[-400:]}
+    rep = json.loads(lines[-1])
+    rep["seconds"] = round(time.perf_counter() - t0, 1)
+    if not rep.get("distinct_gpus", True):
+        rep["note"] = (f"{world} parts on {len(set(devs))} GPU(s) (backend {backend} rehearsal): plumbing only, "
+                       "not an N-GPU rate")
+    return rep
+
+
+def one_gpu_reference(policy, K, P, dev, seed, steps=5, warmup=2) -> dict:
+    """The same round on ONE GPU over the whole model, in the same run (rank 0, after the N-rank timed region):
+    the reference the scaling figures below divide by."""
+    from fedscale_amd.state import ShardGroup
+
+    w = Workload(policy, K, P, 0, 1, dev, seed, ShardGroup(0, 1), budget_fraction=MEM_FRACTION)
+    for _ in range(warmup):
+        w.step()
+    import torch
+
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        w.step()
+    torch.cuda.synchronize(dev)
+    ms = (time.perf_counter() - t0) * 1e3 / steps
+    w.free()
+    return {"ms_per_step": ms, "client_updates_per_s": K / (ms * 1e-3), "steps": steps}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -748,6 +820,7 @@ def main():
     P_local, n_passes = w.P, len(w.passes)
     w_chain = bool(getattr(w, "qf", None) and w.qf.get("chain") is not None)
     w_ld = w.ld
+    split_ms = getattr(w, "split_ms", None)  # FedYoGi: (k_reduce ms, k_yogi_step ms) per step
     # launches of the dominant kernel per step: fa_reduce runs long buckets as column windows (fedagg.hip
     # FA_WINDOWS), so the per-launch figures rocprof reports are the step's divided by this
     from fedscale_amd import kernels as kx
@@ -770,6 +843,17 @@ def main():
                     "c4", CONFIGS["c4"], dev, rank, world, shards, args.seed, args.dist_backend),
                 f"c5_qfedavg_k10000_p100M_x{world}": config_line(
                     "c5", CONFIGS["c5"], dev, rank, world, shards, args.seed, args.dist_backend, steps=2, warmup=1)}
+
+    one_gpu = inproc = None
+    if world > 1 and strong and not args.no_selfcheck:
+        # outside the timed region, the other ranks waiting at the barrier: (1) the same round on one GPU over the
+        # whole model, so the line carries its own scaling reference; (2) the in-process drop-in timed over the
+        # node's GPUs (what a FedScale deployment runs: one aggregator process)
+        _sync_all(dev, world)
+        if rank == 0:
+            one_gpu = one_gpu_reference(policy, K, P, dev, args.seed)
+            inproc = run_inproc_bench(world, K, P, args.dist_backend) if policy == "fedavg" else None
+        dist.barrier()
 
     selfcheck = None
     if world > 1 and not args.no_selfcheck and args.dist_backend == "nccl":
@@ -833,13 +917,26 @@ def main():
                          "alg_bytes_per_launch": alg_bytes / launches, "launches_per_step": launches,
                          "kernel_ms_per_launch": kern_ms_max / launches},
         }
+        if split_ms:
+            res["roofline"]["kernel_ms_split"] = {"k_reduce": split_ms[0], "k_yogi_step": split_ms[1],
+                                                  "k_reduce_launches": launches - 1}
         if world > 1:  # self-checking SCALE records: every rank's kernel time and the process group's size
             res["ranks"] = {"world_process_group": pg_world, "backend": args.dist_backend,
                             "kernel_ms_per_rank": kern_ms_ranks, "kernel_ms_max": kern_ms_max,
                             "kernel_ms_rank0": kern_ms,
                             "roofline_from": "max over ranks of the dominant kernel's mean time per step"}
         if reassembly_ms is not None:
+            # every round ends in egress (aggregator.py:788-804): the model reassembled from the shards
             res["reassembly_ms"] = reassembly_ms
+            res["round_ms_incl_reassembly"] = ms_per_step + reassembly_ms
+            res["value_incl_reassembly"] = K / ((ms_per_step + reassembly_ms) * 1e-3)
+        if one_gpu is not None:
+            res["one_gpu_reference"] = one_gpu
+            res["scaling_vs_one_gpu"] = one_gpu["ms_per_step"] / ms_per_step
+            if reassembly_ms is not None:
+                res["scaling_vs_one_gpu_incl_reassembly"] = one_gpu["ms_per_step"] / (ms_per_step + reassembly_ms)
+        if inproc is not None:
+            res["inproc_drop_in"] = inproc
         if selfcheck is not None:
             res["inproc_multi_gpu_check"] = selfcheck
         if other is not None:

@@ -56,6 +56,12 @@ class ShardedRound:
         for rnd in self.rounds:
             rnd.add(row, **kw)
 
+    def adopt_resident(self, n: int):
+        """Bench hook: ``n`` arrivals already written into every part's staging slots on its device
+        (``DeviceRound.adopt_resident``)."""
+        for rnd in self.rounds:
+            rnd.adopt_resident(n)
+
 
 class ShardedModelAdapter(TorchModelAdapter):
     """``TorchModelAdapter`` whose fp32 bucket is split over ``devices`` (GPU ordinals or torch devices;
@@ -93,6 +99,18 @@ class ShardedModelAdapter(TorchModelAdapter):
     def __reduce__(self):
         return (self.__class__, (self.get_model(), self.optimizer, [d.index for d in self.group.devices], None,
                                  self.group.transport))
+
+    def close(self):
+        """Destroy the device group's RCCL communicator now (its HBM and proxy threads) rather than at interpreter
+        exit, where ``state._LIVE_GROUPS`` would otherwise hold it.  Idempotent; the adapter stays usable (the next
+        collective re-creates the communicator).  Call it from the thread that drives the rounds."""
+        self.group.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
 
     # ---- ingress ----------------------------------------------------------------------------------
     def _stage_row(self, update) -> HostRow:

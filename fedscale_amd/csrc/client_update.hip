@@ -466,6 +466,8 @@ extern "C" int fa_prox_update(float* const* param, const float* const* global, c
   int rc = check_list("fa_prox_update", T, param, global, numel, true);
   if (rc) return rc;
   FA_DEVICE_SCOPE("fa_prox_update", stream, first_ptr(T, (const void* const*)param, numel));
+  FA_TABLE("param", param, numel, T, 4);
+  FA_TABLE("global", global, numel, T, 4);
   int32_t t = 0;
   while (t < T) {
     MtList L;
@@ -496,6 +498,15 @@ static int sgd_groups(const char* what, float* const* param, const float* const*
       return fail(FA_E_ARG, "%s: tensor %d: nesterov needs momentum > 0 and zero dampening", what, i);
   }
   FA_DEVICE_SCOPE(what, stream, first_ptr(T, (const void* const*)param, numel));
+  FA_TABLE("param", param, numel, T, 4);
+  FA_TABLE("grad", grad, numel, T, 4);
+  FA_TABLE("global", global, numel, T, 4);
+  for (int i = 0; momentum_buf && i < T; ++i)  // buffers are read only where the group's momentum != 0
+    if (momentum[i] != 0.f && numel[i] > 0) {
+      char nm[48];
+      snprintf(nm, sizeof(nm), "momentum_buf[%d]", i);
+      FA_OPERAND(nm, momentum_buf[i], (uint64_t)numel[i] * 4);
+    }
   int32_t t = 0;
   while (t < T) {
     SgdList L;
@@ -579,6 +590,10 @@ extern "C" int fa_dp_clip_coef(const float* const* param, const float* const* la
   const int64_t nblk = total_blocks(T, numel);
   if (nblk > INT32_MAX / 2) return fail(FA_E_RANGE, "fa_dp_clip_coef: model too large");
   FA_DEVICE_SCOPE("fa_dp_clip_coef", stream, coef_out);
+  FA_TABLE("param", param, numel, T, 4);
+  FA_TABLE("last", last, numel, T, 4);
+  FA_OPERAND("workspace", workspace, (uint64_t)fa_dp_workspace_bytes(numel, T));
+  FA_OPERAND("coef_out", coef_out, 12);
   double* part = (double*)workspace;
   double* tsum = part + nblk;
   hipStream_t s = (hipStream_t)stream;
@@ -614,6 +629,10 @@ extern "C" int fa_dp_apply(float* const* param, const float* const* last, float*
     if (numel[i] > 0 && (!upload[i] || ((uintptr_t)upload[i] & 3u)))
       return fail(FA_E_ARG, "fa_dp_apply: tensor %d: bad upload pointer", i);
   FA_DEVICE_SCOPE("fa_dp_apply", stream, coef);
+  FA_TABLE("param", param, numel, T, 4);
+  FA_TABLE("last", last, numel, T, 4);
+  if (!scale_only) FA_TABLE("upload", upload, numel, T, 4);
+  FA_OPERAND("coef", coef, 12);
   int32_t t = 0;
   hipStream_t s = (hipStream_t)stream;
   const int wp = (flags & FA_DP_WRITE_PARAM) ? 1 : 0;
@@ -641,6 +660,8 @@ extern "C" int fa_dp_noise_i64(const int64_t* const* x, double* const* out, cons
     if (numel[i] > MT_CHUNK * (int64_t)(INT32_MAX / 4)) return fail(FA_E_RANGE, "fa_dp_noise_i64: tensor %d too large", i);
   }
   FA_DEVICE_SCOPE("fa_dp_noise_i64", stream, first_ptr(T, (const void* const*)out, numel));
+  FA_TABLE("x", x, numel, T, 8);
+  FA_TABLE("out", out, numel, T, 8);
   int32_t t = 0;
   int rc;
   while (t < T) {
@@ -664,6 +685,7 @@ extern "C" int fa_dp_normals(float* out, int64_t n, uint64_t seed, int64_t noise
   if (n < 0 || (n > 0 && !out)) return fail(FA_E_ARG, "fa_dp_normals: bad args");
   if (n == 0) return FA_OK;
   FA_DEVICE_SCOPE("fa_dp_normals", stream, out);
+  FA_OPERAND("out", out, (uint64_t)n * 4);
   int64_t g = (n + 255) / 256;
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(k_dp_normals, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, out, n, seed, noise_offset);

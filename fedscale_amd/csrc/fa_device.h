@@ -9,10 +9,16 @@
 //   * a NULL stream means the legacy default stream of the device that holds the anchor
 //     (hipPointerGetAttributes), which the scope makes current for the call;
 //   * the scope restores the caller's current device on exit, and the launch plan's CU-count and occupancy
-//     queries read the scope's device (fa_scope_device), not whatever device happens to be current.
+//     queries read the scope's device (fa_scope_device), not whatever device happens to be current;
+//   * every other operand is then checked against the scope's device (DevScope::operand / table, FA_OPERAND):
+//     device memory of THAT device, or pinned host memory where the header allows it, and inside its allocation.
+// tests/csrc/ compiles this header against a mock HIP runtime (a table of devices and allocations) to check
+// the wrong-device and pageable cases on the CPU.
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
 
 #include "../../include/fedagg.h"
 
@@ -57,7 +63,7 @@ inline int fa_host_mapped(const void* p) {
 
 class DevScope {
  public:
-  DevScope(const char* what, fa_stream_t stream, const void* anchor) : saved_(fa_t_dev) {
+  DevScope(const char* what, fa_stream_t stream, const void* anchor) : what_(what), saved_(fa_t_dev) {
     if (hipGetDevice(&prev_) != hipSuccess) {
       (void)hipGetLastError();
       rc_ = err(FA_E_HIP, what, "no current HIP device", -1, -1);
@@ -99,6 +105,79 @@ class DevScope {
   int rc() const { return rc_; }
   int device() const { return dev_; }
 
+  // Operand check (round 4): every buffer a launch of this call dereferences must be DEVICE memory of the
+  // scope's device, or — only where the header allows it (host_ok) — pinned host memory the GPU reads at
+  // the same address; and its `bytes` must lie inside the allocation holding it.  Anything else (pageable
+  // memory, another GPU's memory, an undersized buffer) is rejected with FA_E_ARG before the call queues
+  // anything, where the launch would fault the GPU or read over xGMI.  NULL (or bytes == 0) passes: the entry
+  // point checks its required pointers for NULL itself.  Cost: one hipPointerGetAttributes +
+  // hipMemGetAddressRange per allocation (~65 ns each on the MI355X host, tools/ptrattr_probe.hip); pointers
+  // into an allocation this call already checked (a pointer table's tensors share the caching allocator's
+  // segments) cost a range compare.  The checked ranges live for this call only, so a freed and reused
+  // address is always re-queried.
+  int operand(const char* name, const void* p, uint64_t bytes, bool host_ok = false) {
+    if (!p || bytes == 0) return FA_OK;
+    const uintptr_t a = (uintptr_t)p;
+    for (int i = 0; i < nr_; ++i) {  // most recent first: a table's consecutive tensors share a segment
+      const Range& r = rng_[(last_ + nr_ - i) % kRanges];
+      if (a >= r.lo && a < r.hi && (r.host == 0 || host_ok)) {
+        if (bytes > r.hi - a) return operr(name, "%s extends %llu bytes past the end of its allocation", bytes - (r.hi - a));
+        return FA_OK;
+      }
+    }
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+      (void)hipGetLastError();
+      return operr(name, "%s is not memory the GPU can read (unknown to HIP)", 0);
+    }
+    int host = -1;
+    if (at.type == hipMemoryTypeDevice) {
+      if (at.device != dev_) {
+        char m[96];
+        snprintf(m, sizeof(m), "%%s is memory of device %d but the call runs on device %d", at.device, dev_);
+        return operr(name, m, 0);
+      }
+      host = 0;
+    } else if (at.type == hipMemoryTypeHost && at.hostPointer && at.devicePointer == at.hostPointer) {
+      if (!host_ok)
+        return operr(name, "%s is pinned host memory; this operand must be device memory (include/fedagg.h)", 0);
+      host = 1;
+    } else {
+      return operr(name, "%s is pageable (or unmapped) host memory: a kernel reading it would fault the GPU", 0);
+    }
+    void* base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange((hipDeviceptr_t*)&base, &size, (hipDeviceptr_t)p) != hipSuccess || !base) {
+      (void)hipGetLastError();
+      return operr(name, "%s: no allocation range for the pointer", 0);
+    }
+    const Range r{(uintptr_t)base, (uintptr_t)base + size, host};
+    if (a < r.lo || a >= r.hi) return operr(name, "%s lies outside the allocation HIP reports for it", 0);
+    last_ = (last_ + 1) % kRanges;
+    rng_[last_] = r;
+    if (nr_ < kRanges) ++nr_;
+    if (bytes > r.hi - a) return operr(name, "%s extends %llu bytes past the end of its allocation", bytes - (r.hi - a));
+    return FA_OK;
+  }
+  // a HOST table of n device pointers, tensor i holding numel[i] elements of elem_bytes (numel[i] == 0: skipped)
+  int table(const char* name, const void* const* ptrs, const int64_t* numel, int n, int elem_bytes,
+            bool host_ok = false) {
+    if (!ptrs) return FA_OK;
+    char nm[64];
+    for (int i = 0; i < n; ++i) {
+      if (numel[i] <= 0 || !ptrs[i]) continue;
+      const uintptr_t a = (uintptr_t)ptrs[i];
+      const Range& r = rng_[last_];  // fast path: the same segment as the previous tensor
+      if (nr_ > 0 && a >= r.lo && a < r.hi && (r.host == 0 || host_ok) &&
+          (uint64_t)numel[i] * elem_bytes <= r.hi - a)
+        continue;
+      snprintf(nm, sizeof(nm), "%s[%d]", name, i);
+      const int e = operand(nm, ptrs[i], (uint64_t)numel[i] * elem_bytes, host_ok);
+      if (e) return e;
+    }
+    return FA_OK;
+  }
+
  private:
   static int err(int code, const char* what, const char* fmt, int a, int b) {
     char msg[160], buf[256];
@@ -106,6 +185,20 @@ class DevScope {
     snprintf(buf, sizeof(buf), "%s: %s", what, msg);
     return fa_internal_set_error(code, buf);
   }
+  int operr(const char* name, const char* fmt, unsigned long long v) {
+    char msg[200], buf[300];
+    snprintf(msg, sizeof(msg), fmt, name, v);
+    snprintf(buf, sizeof(buf), "%s: %s (nothing was launched)", what_, msg);
+    return fa_internal_set_error(FA_E_ARG, buf);
+  }
+  struct Range {
+    uintptr_t lo, hi;
+    int host;  // 1: pinned host memory
+  };
+  static constexpr int kRanges = 16;
+  Range rng_[kRanges] = {};
+  int nr_ = 0, last_ = 0;
+  const char* what_ = "";
   int prev_ = -1, dev_ = -1, saved_ = -1, rc_ = FA_OK;
 };
 
@@ -113,3 +206,20 @@ class DevScope {
 #define FA_DEVICE_SCOPE(what, stream, anchor) \
   DevScope fa_scope_((what), (stream), (anchor)); \
   if (fa_scope_.rc() != FA_OK) return fa_scope_.rc()
+
+// check an operand of the open scope (fa_scope_) — before the entry point launches anything
+#define FA_OPERAND(name, p, bytes)                                                          \
+  do {                                                                                      \
+    const int fa_e_ = fa_scope_.operand((name), (const void*)(p), (uint64_t)(bytes), false); \
+    if (fa_e_) return fa_e_;                                                                \
+  } while (0)
+#define FA_HOST_OK_OPERAND(name, p, bytes)                                                 \
+  do {                                                                                     \
+    const int fa_e_ = fa_scope_.operand((name), (const void*)(p), (uint64_t)(bytes), true); \
+    if (fa_e_) return fa_e_;                                                               \
+  } while (0)
+#define FA_TABLE(name, ptrs, numel, n, elem_bytes)                                                       \
+  do {                                                                                                   \
+    const int fa_e_ = fa_scope_.table((name), (const void* const*)(ptrs), (numel), (n), (elem_bytes)); \
+    if (fa_e_) return fa_e_;                                                                             \
+  } while (0)

@@ -57,6 +57,12 @@ static int check_launch(const char* what) {
   return FA_OK;
 }
 static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+// bytes a kernel touches in a client-major [K][ld] buffer of P columns (float4 columns past P included) and in
+// a per-column vector (operand extents for DevScope::operand)
+static uint64_t rows_bytes(int64_t K, int64_t ld, int64_t P, int elem = 4) {
+  return K > 0 ? (uint64_t)((K - 1) * ld + (P + 3) / 4 * 4) * elem : 0;
+}
+static uint64_t cols_bytes(int64_t P) { return (uint64_t)((P + 3) / 4) * 16; }
 
 // shared with the other translation units of the library (client_update.hip)
 extern "C" __attribute__((visibility("hidden"))) int fa_internal_set_error(int code, const char* msg) {
@@ -625,12 +631,14 @@ extern "C" int fa_reduce(const float* x, int64_t ld, int32_t K, int64_t P, const
   int e = check_reduce_args("fa_reduce", x, ld, K, P, acc_in, out, flags);
   if (e) return e;
   if (P == 0) return FA_OK;
-  if (K > 0 && fa_host_mapped(x) < 0)
-    return fail(FA_E_ARG, "fa_reduce: x must be device memory or pinned host memory mapped for the GPU");
   RedArgs r{};
   r.x = x; r.ld4 = ld / 4; r.P4 = (P + 3) / 4; r.K = K; r.flags = flags; r.a = a; r.acc_in = acc_in;
   r.out = out; r.denom = denom;
   FA_DEVICE_SCOPE("fa_reduce", stream, out);
+  FA_HOST_OK_OPERAND("x", x, rows_bytes(K, ld, P));  // device, or pinned host (the zero-copy round)
+  FA_OPERAND("a", a, (uint64_t)K * 4);
+  FA_OPERAND("acc_in", (flags & FA_ACCUMULATE) ? acc_in : nullptr, cols_bytes(P));
+  FA_OPERAND("out", out, cols_bytes(P));
   hipStream_t st = (hipStream_t)stream;
   if (flags & FA_FINALIZE) return launch_reduce<EPI_MEAN>(r, st, "fa_reduce");
   return launch_reduce<EPI_CHAIN>(r, st, "fa_reduce");
@@ -644,13 +652,15 @@ extern "C" int fa_reduce_mirror(const float* x, int64_t ld, int32_t K, int64_t P
   if (!(flags & FA_FINALIZE)) return fail(FA_E_ARG, "fa_reduce_mirror: needs FA_FINALIZE");
   if (!mirror || !aligned16(mirror)) return fail(FA_E_ARG, "fa_reduce_mirror: mirror NULL or not 16-byte aligned");
   if (P == 0) return FA_OK;
-  if (fa_host_mapped(x) < 0 || fa_host_mapped(mirror) < 0)
-    return fail(FA_E_ARG, "fa_reduce_mirror: x and mirror must be device memory or pinned host memory mapped for "
-                          "the GPU (pageable memory would fault it)");
   RedArgs r{};
   r.x = x; r.ld4 = ld / 4; r.P4 = (P + 3) / 4; r.K = K; r.flags = flags; r.a = a; r.acc_in = acc_in;
   r.out = out; r.denom = denom; r.mean_out = mirror;
   FA_DEVICE_SCOPE("fa_reduce_mirror", stream, out);
+  FA_HOST_OK_OPERAND("x", x, rows_bytes(K, ld, P));
+  FA_HOST_OK_OPERAND("mirror", mirror, cols_bytes(P));
+  FA_OPERAND("a", a, (uint64_t)K * 4);
+  FA_OPERAND("acc_in", (flags & FA_ACCUMULATE) ? acc_in : nullptr, cols_bytes(P));
+  FA_OPERAND("out", out, cols_bytes(P));
   return launch_reduce<EPI_MEAN>(r, (hipStream_t)stream, "fa_reduce_mirror");
 }
 
@@ -665,6 +675,14 @@ extern "C" int fa_reduce_yogi(const float* x, int64_t ld, int32_t K, int64_t P, 
     return fail(FA_E_ARG, "fa_reduce_yogi: last/m/v must be 16-byte aligned");
   if (P == 0) return FA_OK;
   FA_DEVICE_SCOPE("fa_reduce_yogi", stream, out);
+  FA_OPERAND("x", x, rows_bytes(K, ld, P));
+  FA_OPERAND("a", a, (uint64_t)K * 4);
+  FA_OPERAND("acc_in", (flags & FA_ACCUMULATE) ? acc_in : nullptr, cols_bytes(P));
+  FA_OPERAND("last", last, cols_bytes(P));
+  FA_OPERAND("m", m, cols_bytes(P));
+  FA_OPERAND("v", v, cols_bytes(P));
+  FA_OPERAND("out", out, cols_bytes(P));
+  FA_OPERAND("mean_out", mean_out, cols_bytes(P));
   RedArgs r{};
   r.x = x; r.ld4 = ld / 4; r.P4 = (P + 3) / 4; r.K = K; r.flags = flags; r.a = a; r.acc_in = acc_in;
   r.out = out; r.denom = denom; r.last = last; r.m = m; r.v = v; r.mean_out = mean_out;
@@ -704,6 +722,11 @@ extern "C" int fa_yogi_step(const float* cur, const float* last, float* m, float
   if (!aligned16(cur) || !aligned16(last) || !aligned16(m) || !aligned16(v) || !aligned16(out))
     return fail(FA_E_ARG, "fa_yogi_step: pointers must be 16-byte aligned");
   FA_DEVICE_SCOPE("fa_yogi_step", stream, out);
+  FA_OPERAND("cur", cur, cols_bytes(P));
+  FA_OPERAND("last", last, cols_bytes(P));
+  FA_OPERAND("m", m, cols_bytes(P));
+  FA_OPERAND("v", v, cols_bytes(P));
+  FA_OPERAND("out", out, cols_bytes(P));
   const int64_t P4 = (P + 3) / 4;
   hipLaunchKernelGGL(k_yogi_step, dim3(stride_grid(P4)), dim3(256), 0, (hipStream_t)stream,
                      (const f4*)cur, (const f4*)last, (f4*)m, (f4*)v, (f4*)out, P4, eta, tau, beta, omb, omb2,
@@ -1530,6 +1553,13 @@ extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t
     return fail(FA_E_ARG, "fa_qfed_accumulate: x/last/delta/chain must be 16-byte aligned");
   if (!(lr > 1e-30f && lr < 1e30f)) return fail(FA_E_ARG, "fa_qfed_accumulate: lr=%g outside (1e-30, 1e30)", (double)lr);
   FA_DEVICE_SCOPE("fa_qfed_accumulate", stream, delta);
+  FA_OPERAND("x", x, rows_bytes(K, ld, P));
+  FA_OPERAND("last", last, cols_bytes(P));
+  FA_OPERAND("alpha", alpha, (uint64_t)K * 4);
+  FA_OPERAND("delta", delta, cols_bytes(P));
+  FA_OPERAND("chain", chain, cols_bytes(P));
+  FA_OPERAND("sqnorm", sqnorm, (uint64_t)K * 8);
+  FA_OPERAND("workspace", workspace, (uint64_t)workspace_bytes);
   hipStream_t st = (hipStream_t)stream;
   const int fast = (lr >= 9.5367432e-07f && lr <= 1048576.f) ? 1 : 0;  // [2^-20, 2^20]
   const int kern = chain ? QF_CHAIN_KERNEL : QF_KERNEL;
@@ -1577,6 +1607,10 @@ extern "C" int fa_qfed_hs(const double* sqnorm, const float* c1, const float* c2
                           fa_stream_t stream) {
   if (K < 0 || !sqnorm || !c1 || !c2 || !hs_out) return fail(FA_E_ARG, "fa_qfed_hs: bad arguments");
   FA_DEVICE_SCOPE("fa_qfed_hs", stream, hs_out);
+  FA_OPERAND("sqnorm", sqnorm, (uint64_t)K * 8);
+  FA_OPERAND("c1", c1, (uint64_t)K * 4);
+  FA_OPERAND("c2", c2, (uint64_t)K * 4);
+  FA_OPERAND("hs_out", hs_out, 8);
   hipLaunchKernelGGL(k_qfed_hs, dim3(1), dim3(256), 0, (hipStream_t)stream, sqnorm, c1, c2, (int)K, hs_out);
   return check_launch("fa_qfed_hs");
 }
@@ -1602,6 +1636,10 @@ extern "C" int fa_qfed_finalize(const float* last, const float* delta, const flo
     return fail(FA_E_ARG, "fa_qfed_finalize: pointers must be 16-byte aligned");
   if (P == 0) return FA_OK;
   FA_DEVICE_SCOPE("fa_qfed_finalize", stream, out);
+  FA_OPERAND("last", last, cols_bytes(P));
+  FA_OPERAND("delta", delta, cols_bytes(P));
+  FA_OPERAND("hs_dev", hs_dev, 8);
+  FA_OPERAND("out", out, cols_bytes(P));
   const int64_t P4 = (P + 3) / 4;
   hipLaunchKernelGGL(k_qfed_finalize, dim3(stride_grid(P4)), dim3(256), 0, (hipStream_t)stream,
                      (const f4*)last, (const f4*)delta, hs_dev, (f4*)out, P4);
@@ -1622,6 +1660,8 @@ extern "C" int fa_sum_rows_f64(const double* x, int64_t ld, int32_t n, int64_t K
   if (n < 1 || K < 0 || ld < K || !x || !out) return fail(FA_E_ARG, "fa_sum_rows_f64: bad arguments");
   if (K == 0) return FA_OK;
   FA_DEVICE_SCOPE("fa_sum_rows_f64", stream, out);
+  FA_OPERAND("x", x, (uint64_t)((n - 1) * ld + K) * 8);
+  FA_OPERAND("out", out, (uint64_t)K * 8);
   hipLaunchKernelGGL(k_sum_rows_f64, dim3(stride_grid(K)), dim3(256), 0, (hipStream_t)stream, x, ld, (int)n, K, out);
   return check_launch("fa_sum_rows_f64");
 }
@@ -1654,9 +1694,10 @@ extern "C" int fa_side_accumulate(const int64_t* xi, int32_t ldq, int32_t K, int
   if (mode == 1 && (!acc_d || !w)) return fail(FA_E_ARG, "fa_side_accumulate: acc_d/w NULL");
   if (mode != 0 && mode != 1) return fail(FA_E_ARG, "fa_side_accumulate: mode %d", (int)mode);
   if (K == 0) return FA_OK;
-  if (fa_host_mapped(xi) < 0)
-    return fail(FA_E_ARG, "fa_side_accumulate: xi must be device memory or pinned host memory mapped for the GPU");
   FA_DEVICE_SCOPE("fa_side_accumulate", stream, mode == 0 ? (const void*)acc_i : (const void*)acc_d);
+  FA_HOST_OK_OPERAND("xi", xi, (uint64_t)((int64_t)(K - 1) * ldq + Q) * 8);  // device, or the pinned mirror
+  FA_OPERAND("w", mode == 1 ? w : nullptr, (uint64_t)K * 8);
+  FA_OPERAND(mode == 0 ? "acc_i" : "acc_d", mode == 0 ? (const void*)acc_i : (const void*)acc_d, (uint64_t)Q * 8);
   hipLaunchKernelGGL(k_side_accum, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, xi, ldq, K, Q, mode, w,
                      acc_i, acc_d, (flags & FA_ACCUMULATE) ? 1 : 0);
   return check_launch("fa_side_accumulate");
@@ -1676,6 +1717,9 @@ extern "C" int fa_side_close(const int64_t* acc_i, const double* acc_d, int32_t 
   if (Q == 0) return FA_OK;
   if (Q < 0 || (mode == 0 && !acc_i) || (mode == 1 && !acc_d)) return fail(FA_E_ARG, "fa_side_close: bad args");
   FA_DEVICE_SCOPE("fa_side_close", stream, mode == 0 ? (const void*)acc_i : (const void*)acc_d);
+  FA_OPERAND(mode == 0 ? "acc_i" : "acc_d", mode == 0 ? (const void*)acc_i : (const void*)acc_d, (uint64_t)Q * 8);
+  FA_OPERAND("cur", cur, (uint64_t)Q * 8);
+  FA_OPERAND("model", model, (uint64_t)Q * 8);
   hipLaunchKernelGGL(k_side_close, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, acc_i, acc_d, Q, mode,
                      denom, cur, model);
   return check_launch("fa_side_close");
@@ -1707,6 +1751,12 @@ extern "C" int fa_side_yogi(const double* cur, const int64_t* last, double* m, d
   if (Q == 0) return FA_OK;
   if (Q < 0 || !cur || !m || !v) return fail(FA_E_ARG, "fa_side_yogi: bad args");
   FA_DEVICE_SCOPE("fa_side_yogi", stream, m);
+  FA_OPERAND("cur", cur, (uint64_t)Q * 8);
+  FA_OPERAND("last", last, (uint64_t)Q * 8);
+  FA_OPERAND("m", m, (uint64_t)Q * 8);
+  FA_OPERAND("v", v, (uint64_t)Q * 8);
+  FA_OPERAND("step", step, (uint64_t)Q * 8);
+  FA_OPERAND("model", model, (uint64_t)Q * 8);
   hipLaunchKernelGGL(k_side_yogi, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, cur, last, m, v, step,
                      model, Q, eta, tau, beta, omb, omb2, (flags & FA_YOGI_INIT) ? 1 : 0);
   return check_launch("fa_side_yogi");
@@ -1750,6 +1800,11 @@ extern "C" int fa_side_qfed_accumulate(const int64_t* xi, int32_t ldq, int32_t K
   if (Q < 0 || K < 0 || ldq < Q || !xi || !last || !alpha || !delta_s || !sqnorm)
     return fail(FA_E_ARG, "fa_side_qfed_accumulate: bad args");
   FA_DEVICE_SCOPE("fa_side_qfed_accumulate", stream, delta_s);
+  FA_OPERAND("xi", xi, (uint64_t)((int64_t)(K - 1) * ldq + Q) * 8);
+  FA_OPERAND("last", last, (uint64_t)Q * 8);
+  FA_OPERAND("alpha", alpha, (uint64_t)K * 4);
+  FA_OPERAND("delta_s", delta_s, (uint64_t)Q * 4);
+  FA_OPERAND("sqnorm", sqnorm, (uint64_t)K * 8);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(k_side_qfed_delta, dim3((Q + 63) / 64), dim3(64), 0, st, xi, ldq, K, Q, last, alpha, lr, delta_s,
                      (flags & FA_ACCUMULATE) ? 1 : 0);
@@ -1771,6 +1826,10 @@ extern "C" int fa_side_qfed_finalize(const int64_t* last, const float* delta_s, 
   if (Q == 0) return FA_OK;
   if (Q < 0 || !last || !delta_s || !hs_dev || !model) return fail(FA_E_ARG, "fa_side_qfed_finalize: bad args");
   FA_DEVICE_SCOPE("fa_side_qfed_finalize", stream, model);
+  FA_OPERAND("last", last, (uint64_t)Q * 8);
+  FA_OPERAND("delta_s", delta_s, (uint64_t)Q * 4);
+  FA_OPERAND("hs_dev", hs_dev, 8);
+  FA_OPERAND("model", model, (uint64_t)Q * 8);
   hipLaunchKernelGGL(k_side_qfed_finalize, dim3((Q + 63) / 64), dim3(64), 0, (hipStream_t)stream, last, delta_s,
                      hs_dev, model, Q);
   return check_launch("fa_side_qfed_finalize");
@@ -1810,6 +1869,7 @@ extern "C" int fa_fill_synthetic(float* x, int64_t ld, int32_t K, int64_t P, uin
   if (K == 0 || ld == 0) return FA_OK;
   if (K > 65535) return fail(FA_E_RANGE, "fa_fill_synthetic: K=%d > 65535 per call", (int)K);
   FA_DEVICE_SCOPE("fa_fill_synthetic", stream, x);
+  FA_OPERAND("x", x, (uint64_t)K * ld * 4);
   int64_t gx = (ld + 255) / 256;
   if (gx > 2048) gx = 2048;
   hipLaunchKernelGGL(k_fill, dim3((unsigned)gx, (unsigned)K), dim3(256), 0, (hipStream_t)stream, x, ld, K, P, seed, k0,
@@ -2040,6 +2100,13 @@ extern "C" int fa_prefix_box_combine(const float* xs, const int64_t* desc, int32
     return fail(FA_E_ARG, "fa_prefix_box_combine: NULL pointer");
   if (!aligned16(xs)) return fail(FA_E_ARG, "fa_prefix_box_combine: xs must be 16-byte aligned");
   FA_DEVICE_SCOPE("fa_prefix_box_combine", stream, xs);
+  // (the boxes' extents live in desc on the device: xs and global are checked at their base)
+  FA_OPERAND("xs", xs, 16);
+  FA_OPERAND("desc", desc, (uint64_t)K * T * 4 * 8);
+  FA_OPERAND("tensors", tensors, (uint64_t)T * 4 * 8);
+  FA_OPERAND("chunk_tensor", chunk_tensor, (uint64_t)nchunks * 2 * 4);
+  FA_OPERAND("chunk_first", chunk_first, (uint64_t)nchunks * 8);
+  FA_OPERAND("global", global, 4);
   const int grid = (HB_GRID > 0 && nchunks > HB_GRID) ? HB_GRID : nchunks;
   hipLaunchKernelGGL(k_prefix_box, dim3(grid), dim3(256), 0, (hipStream_t)stream, xs, desc, (int)K, (int)T, tensors,
                      chunk_tensor, chunk_first, global, (int)nchunks);

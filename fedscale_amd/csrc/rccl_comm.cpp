@@ -22,8 +22,7 @@
 #include <rccl/rccl.h>
 
 #include "../../include/fedagg.h"
-
-extern "C" __attribute__((visibility("hidden"))) int fa_internal_set_error(int code, const char* msg);
+#include "fa_device.h"
 
 namespace {
 
@@ -128,6 +127,28 @@ int check_streams(const Comm* c, void* const* streams, const char* what) {
   return FA_OK;
 }
 
+// the buffer of rank i (bytes of it) must be device memory of the communicator's device i (fa_device.h): a
+// buffer on another GPU would be read over xGMI by the wrong rank's kernels, pageable memory would fault the GPU
+int check_buf(const Comm* c, const char* what, void* const* streams, int i, const char* name, const void* p,
+              uint64_t bytes) {
+  if (!p) {
+    char buf[160];
+    snprintf(buf, sizeof(buf), "%s: %s[%d] is NULL", what, name, i);
+    return fa_internal_set_error(FA_E_ARG, buf);
+  }
+  DevScope scope(what, streams[i], p);
+  if (scope.rc() != FA_OK) return scope.rc();
+  if (scope.device() != c->devs[i]) {
+    char buf[200];
+    snprintf(buf, sizeof(buf), "%s: %s[%d] is memory of device %d, the communicator's rank %d is device %d", what,
+             name, i, scope.device(), i, c->devs[i]);
+    return fa_internal_set_error(FA_E_ARG, buf);
+  }
+  char nm[48];
+  snprintf(nm, sizeof(nm), "%s[%d]", name, i);
+  return scope.operand(nm, p, bytes);
+}
+
 // one grouped launch: op(i) issues device i's part of the collective
 template <class F>
 int grouped(const Comm* c, const char* what, F op) {
@@ -196,6 +217,10 @@ extern "C" int fa_rccl_all_gather(void* comm, const void* const* send, void* con
   if ((e = dtype_of(dtype, &dt, &sz))) return e;
   if (!send || !recv || !streams) return fa_internal_set_error(FA_E_ARG, "fa_rccl_all_gather: NULL table");
   if ((e = check_streams(c, streams, "fa_rccl_all_gather"))) return e;
+  for (int i = 0; i < c->n && count > 0; ++i)
+    if ((e = check_buf(c, "fa_rccl_all_gather", streams, i, "send", send[i], (uint64_t)count * sz)) ||
+        (e = check_buf(c, "fa_rccl_all_gather", streams, i, "recv", recv[i], (uint64_t)count * sz * c->n)))
+      return e;
   const RcclApi* a = api();
   return grouped(c, "fa_rccl_all_gather", [&](int i) {
     return a->all_gather(send[i], recv[i], (size_t)count, dt, c->comms[i], (hipStream_t)streams[i]);
@@ -212,6 +237,10 @@ extern "C" int fa_rccl_all_reduce(void* comm, const void* const* send, void* con
   if ((e = dtype_of(dtype, &dt, &sz))) return e;
   if (!send || !recv || !streams) return fa_internal_set_error(FA_E_ARG, "fa_rccl_all_reduce: NULL table");
   if ((e = check_streams(c, streams, "fa_rccl_all_reduce"))) return e;
+  for (int i = 0; i < c->n && count > 0; ++i)
+    if ((e = check_buf(c, "fa_rccl_all_reduce", streams, i, "send", send[i], (uint64_t)count * sz)) ||
+        (e = check_buf(c, "fa_rccl_all_reduce", streams, i, "recv", recv[i], (uint64_t)count * sz)))
+      return e;
   const RcclApi* a = api();
   return grouped(c, "fa_rccl_all_reduce", [&](int i) {
     return a->all_reduce(send[i], recv[i], (size_t)count, dt, ncclSum, c->comms[i], (hipStream_t)streams[i]);
@@ -229,6 +258,12 @@ extern "C" int fa_rccl_gather(void* comm, const void* const* send, void* recv_ro
   if (!send || !recv_root || !streams || root < 0 || root >= c->n)
     return fa_internal_set_error(FA_E_ARG, "fa_rccl_gather: bad root or NULL table");
   if ((e = check_streams(c, streams, "fa_rccl_gather"))) return e;
+  for (int i = 0; i < c->n && count > 0; ++i)
+    if ((e = check_buf(c, "fa_rccl_gather", streams, i, "send", send[i], (uint64_t)count * sz)))
+      return e;
+  if (count > 0 && (e = check_buf(c, "fa_rccl_gather", streams, root, "recv_root", recv_root,
+                                  (uint64_t)count * sz * c->n)))
+    return e;
   const RcclApi* a = api();
   return grouped(c, "fa_rccl_gather", [&](int i) {
     return a->gather(send[i], i == root ? recv_root : nullptr, (size_t)count, dt, root, c->comms[i],
@@ -247,6 +282,8 @@ extern "C" int fa_rccl_broadcast(void* comm, void* const* bufs, int64_t count, i
   if (!bufs || !streams || root < 0 || root >= c->n)
     return fa_internal_set_error(FA_E_ARG, "fa_rccl_broadcast: bad root or NULL table");
   if ((e = check_streams(c, streams, "fa_rccl_broadcast"))) return e;
+  for (int i = 0; i < c->n && count > 0; ++i)
+    if ((e = check_buf(c, "fa_rccl_broadcast", streams, i, "bufs", bufs[i], (uint64_t)count * sz))) return e;
   const RcclApi* a = api();
   return grouped(c, "fa_rccl_broadcast", [&](int i) {
     return a->broadcast(bufs[i], bufs[i], (size_t)count, dt, root, c->comms[i], (hipStream_t)streams[i]);

@@ -166,6 +166,21 @@ class DeviceRound:
         self.n += 1
         self.n_local += 1
 
+    def adopt_resident(self, n: int):
+        """Bench hook (FedAvg): take ``n`` arrivals whose updates are ALREADY in the staging slots
+        [slot, slot + n), written there on the device (``synth.fill`` on ``staging.x``), as ``add`` would have
+        staged them — the device-resident round ``fedscale_amd.inproc_bench`` times, without host ingress (the
+        same resident-input convention as bench.py's SPMD workload).  Their side-table rows are the staging's
+        (zero unless written)."""
+        if self.policy != "fedavg" or self.cg is not None:
+            raise ValueError("adopt_resident: FedAvg rounds of a whole-model or parameter-sharded layout only")
+        if n < 0 or self.slot + n > self.cap or self.n + n > self.K:
+            raise ValueError(f"adopt_resident: {n} arrivals do not fit (slot {self.slot} of {self.cap}, "
+                             f"{self.n} of K={self.K})")
+        self.slot += n
+        self.n += n
+        self.n_local += n
+
     def _qfed_scalars(self, k, loss, lr, q):
         """Per-client scalars of optimizers.py:87-98, computed in double exactly as the reference does."""
         base = loss + 1e-10

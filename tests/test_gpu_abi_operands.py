@@ -1,0 +1,272 @@
+"""Every launching entry point of the C ABI checks every operand before it queues anything (fa_device.h,
+DevScope::operand / table): a pageable host buffer handed in any operand position returns FA_E_ARG, names
+the operand, and leaves every output untouched; pinned host memory is accepted only where include/fedagg.h
+allows it (the zero-copy round's x / mirror / xi).  Called straight through ctypes (no Python wrapper
+validation in between).  The wrong-device half of the check is covered on the CPU against a mock runtime
+(tests/test_abi_operands.py): the box has one GPU."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+K, LD, P, Q = 4, 64, 60, 3
+FIN, ACC = 2, 1
+
+
+def _u64(ptrs):
+    return np.asarray(ptrs, dtype=np.uint64)
+
+
+class Case:
+    """An entry point, its operands (device tensors, or lists of them for pointer tables), the operands a
+    launch writes, and how the ABI arguments are formed from a {name: pointer or [pointers]} map."""
+
+    def __init__(self, name, ops, outs, args, host_ok=()):
+        self.name, self.ops, self.outs, self.args, self.host_ok = name, ops, outs, args, set(host_ok)
+
+
+def _cases(dev, st):
+    def f(n, v=7.0, dt=torch.float32):
+        return torch.full((n,), v, dtype=dt, device=dev)
+
+    x = f(K * LD, 0.5)
+    hp = [ctypes.c_float(3e-3), ctypes.c_float(1e-8), ctypes.c_float(0.9), ctypes.c_float(0.1), ctypes.c_float(0.01)]
+    from fedscale_amd import _native as N
+
+    lib = N.load()
+    ws_q = lib.fa_qfed_workspace_bytes(K, LD, P)
+    numel = np.asarray([40, 24], dtype=np.int64)
+    ws_dp = lib.fa_dp_workspace_bytes(numel.ctypes.data, 2)
+    tab = lambda v: [f(40, v), f(24, v)]  # noqa: E731 (a two-tensor model)
+    tab64 = lambda v, dt: [f(40, v, dt), f(24, v, dt)]  # noqa: E731
+    keep = []  # host arrays whose addresses are in flight
+
+    def t(ps):
+        a = _u64(ps)
+        keep.append(a)
+        return a.ctypes.data
+
+    def host(dt, vals):  # a host array of per-tensor scalars (read by the host, never by a kernel)
+        a = np.asarray(vals, dtype=dt)
+        keep.append(a)
+        return a.ctypes.data
+
+    box_desc = torch.tensor([[0, 1, 4, 4]] * K, dtype=torch.int64, device=dev).reshape(-1)
+    cases = [
+        Case("fa_reduce", dict(x=x, a=f(K, 1.0), acc_in=f(LD, 0.0), out=f(LD)), ["out"],
+             lambda p: (p["x"], LD, K, P, p["a"], p["acc_in"], p["out"], ctypes.c_float(4.0), FIN | ACC, st),
+             host_ok=["x"]),
+        Case("fa_reduce_mirror", dict(x=x, a=f(K, 1.0), acc_in=f(LD, 0.0), out=f(LD), mirror=f(LD)), ["out", "mirror"],
+             lambda p: (p["x"], LD, K, P, p["a"], p["acc_in"], p["out"], p["mirror"], ctypes.c_float(4.0), FIN | ACC,
+                        st), host_ok=["x", "mirror"]),
+        Case("fa_reduce_yogi", dict(x=x, a=f(K, 1.0), acc_in=f(LD, 0.0), last=f(LD), m=f(LD), v=f(LD), out=f(LD),
+                                    mean_out=f(LD)), ["m", "v", "out", "mean_out"],
+             lambda p: (p["x"], LD, K, P, p["a"], p["acc_in"], ctypes.c_float(4.0), p["last"], p["m"], p["v"], p["out"],
+                        p["mean_out"], *hp, FIN | ACC, st)),
+        Case("fa_yogi_step", dict(cur=f(LD), last=f(LD), m=f(LD), v=f(LD), out=f(LD)), ["m", "v", "out"],
+             lambda p: (p["cur"], p["last"], p["m"], p["v"], p["out"], P, *hp, 0, st)),
+        Case("fa_qfed_accumulate", dict(x=x, last=f(LD), alpha=f(K, 1.0), delta=f(LD), chain=f(LD),
+                                        sqnorm=f(K, 0.0, torch.float64), workspace=f(ws_q // 8 + 1, 0.0, torch.float64)),
+             ["delta", "chain", "sqnorm"],
+             lambda p: (p["x"], LD, K, P, p["last"], p["alpha"], ctypes.c_float(0.05), p["delta"], p["chain"],
+                        p["sqnorm"], p["workspace"], ws_q, ACC, st)),
+        Case("fa_qfed_hs", dict(sqnorm=f(K, 1.0, torch.float64), c1=f(K, 1.0), c2=f(K, 1.0), hs_out=f(2)), ["hs_out"],
+             lambda p: (p["sqnorm"], p["c1"], p["c2"], K, p["hs_out"], st)),
+        Case("fa_qfed_finalize", dict(last=f(LD), delta=f(LD), hs=f(2, 2.0), out=f(LD)), ["out"],
+             lambda p: (p["last"], p["delta"], p["hs"], p["out"], P, st)),
+        Case("fa_sum_rows_f64", dict(x=f(2 * K, 1.0, torch.float64), out=f(K, 0.0, torch.float64)), ["out"],
+             lambda p: (p["x"], K, 2, K, p["out"], st)),
+        Case("fa_side_accumulate", dict(xi=f(K * Q, 3, torch.int64), w=f(K, 1.0, torch.float64),
+                                        acc_d=f(Q, 9.0, torch.float64)), ["acc_d"],
+             lambda p: (p["xi"], Q, K, Q, 1, p["w"], None, p["acc_d"], 0, st), host_ok=["xi"]),
+        Case("fa_side_close", dict(acc_i=f(Q, 8, torch.int64), cur=f(Q, 0.0, torch.float64),
+                                   model=f(Q, 5, torch.int64)), ["cur", "model"],
+             lambda p: (p["acc_i"], None, Q, 0, ctypes.c_double(4.0), p["cur"], p["model"], st)),
+        Case("fa_side_yogi", dict(cur=f(Q, 1.0, torch.float64), last=f(Q, 1, torch.int64), m=f(Q, 0.0, torch.float64),
+                                  v=f(Q, 0.0, torch.float64), step=f(Q, 0.0, torch.float64), model=f(Q, 5, torch.int64)),
+             ["m", "v", "step", "model"],
+             lambda p: (p["cur"], p["last"], p["m"], p["v"], p["step"], p["model"], Q, *[ctypes.c_double(h.value)
+                                                                                         for h in hp], 0, st)),
+        Case("fa_side_qfed_accumulate", dict(xi=f(K * Q, 3, torch.int64), last=f(Q, 1, torch.int64),
+                                             alpha=f(K, 1.0), delta_s=f(Q), sqnorm=f(K, 0.0, torch.float64)),
+             ["delta_s", "sqnorm"],
+             lambda p: (p["xi"], Q, K, Q, p["last"], p["alpha"], ctypes.c_float(0.05), p["delta_s"], p["sqnorm"], 0,
+                        st)),
+        Case("fa_side_qfed_finalize", dict(last=f(Q, 1, torch.int64), delta_s=f(Q), hs=f(2, 2.0),
+                                           model=f(Q, 5, torch.int64)), ["model"],
+             lambda p: (p["last"], p["delta_s"], p["hs"], p["model"], Q, st)),
+        Case("fa_fill_synthetic", dict(x=f(K * LD)), ["x"],
+             lambda p: (p["x"], LD, K, P, 1, 0, ctypes.c_float(0.05), ctypes.c_float(0.01), st)),
+        Case("fa_prefix_box_combine",
+             dict(xs=f(K * 16, 1.0), desc=box_desc + 0, tensors=torch.tensor([0, 1, 4, 1], dtype=torch.int64,
+                                                                               device=dev),
+                  chunk_tensor=torch.tensor([0, -1], dtype=torch.int32, device=dev),
+                  chunk_first=torch.tensor([0], dtype=torch.int64, device=dev), glob=f(4)), ["glob"],
+             lambda p: (p["xs"], p["desc"], K, p["tensors"], 1, p["chunk_tensor"], p["chunk_first"], 1, p["glob"], st)),
+        Case("fa_dp_normals", dict(out=f(64)), ["out"], lambda p: (p["out"], 64, 5, 0, st)),
+        # client-side pointer tables (include/fedclient.h)
+        Case("fa_prox_update", dict(param=tab(1.0), glob=tab(2.0)), ["param"],
+             lambda p: (t(p["param"]), t(p["glob"]), numel.ctypes.data, 2, ctypes.c_float(0.1), st)),
+        Case("fa_sgd_prox_step", dict(param=tab(1.0), grad=tab(0.5), buf=tab(0.0), glob=tab(2.0)), ["param", "buf"],
+             lambda p: (t(p["param"]), t(p["grad"]), t(p["buf"]), t(p["glob"]), numel.ctypes.data, 2,
+                        ctypes.c_float(0.1), ctypes.c_float(0.9), ctypes.c_double(0.0), ctypes.c_float(5e-4), 0, 0,
+                        ctypes.c_float(0.01), 1, st)),
+        Case("fa_sgd_prox_step_groups", dict(param=tab(1.0), grad=tab(0.5), buf=tab(0.0), glob=tab(2.0)),
+             ["param", "buf"],
+             lambda p: (t(p["param"]), t(p["grad"]), t(p["buf"]), t(p["glob"]), numel.ctypes.data, 2,
+                        host(np.float32, [0.1, 0.2]), host(np.float32, [0.9, 0.9]), host(np.float64, [0.0, 0.0]),
+                        host(np.float32, [5e-4, 0.0]), host(np.int32, [0, 0]), ctypes.c_float(0.01), 1, st)),
+        Case("fa_dp_clip_coef", dict(param=tab(1.0), last=tab(0.5), workspace=f(ws_dp // 8 + 1, 0.0, torch.float64),
+                                     coef=f(3)), ["coef"],
+             lambda p: (t(p["param"]), t(p["last"]), numel.ctypes.data, 2, ctypes.c_float(1.0), 0, p["workspace"],
+                        p["coef"], st)),
+        Case("fa_dp_apply", dict(param=tab(1.0), last=tab(0.5), upload=tab(0.0), coef=f(3, 0.5)), ["param", "upload"],
+             lambda p: (t(p["param"]), t(p["last"]), t(p["upload"]), numel.ctypes.data, t([0, 40]), 2, p["coef"],
+                        ctypes.c_float(0.1), 3, 1, st)),
+        Case("fa_dp_noise_i64", dict(x=tab64(3, torch.int64), out=tab64(0.0, torch.float64)), ["out"],
+             lambda p: (t(p["x"]), t(p["out"]), numel.ctypes.data, t([0, 40]), 2, ctypes.c_float(0.1), 3, st)),
+    ]
+    return cases, keep
+
+
+def _ptrs(ops, bad_name=None, bad_ptr=None, bad_index=0):
+    p = {}
+    for n, v in ops.items():
+        if isinstance(v, list):
+            p[n] = [x.data_ptr() for x in v]
+            if n == bad_name:
+                p[n][bad_index] = bad_ptr
+        else:
+            p[n] = bad_ptr if n == bad_name else v.data_ptr()
+    return p
+
+
+def _snapshot(case):
+    out = {}
+    for n in case.outs:
+        v = case.ops[n]
+        out[n] = [x.clone() for x in v] if isinstance(v, list) else v.clone()
+    return out
+
+
+def _unchanged(case, snap):
+    torch.cuda.synchronize()
+    for n, want in snap.items():
+        got = case.ops[n]
+        if isinstance(got, list):
+            assert all(torch.equal(a, b) for a, b in zip(got, want)), f"{case.name}: {n} was written"
+        else:
+            assert torch.equal(got, want), f"{case.name}: {n} was written"
+
+
+def test_pageable_operand_in_every_position_is_rejected_before_any_launch(gpu_device):
+    from fedscale_amd import _native as N
+
+    lib = N.load()
+    st = torch.cuda.current_stream().cuda_stream
+    pageable = np.zeros(1 << 20, dtype=np.float64)  # plain malloc'd host memory: pageable
+    bad = pageable.ctypes.data
+    cases, keep = _cases(gpu_device, st)
+    exported = {n for n in N.SIGNATURES}
+    checked = set()
+    for case in cases:
+        assert case.name in exported
+        fn = getattr(lib, case.name)
+        for name, v in case.ops.items():
+            snap = _snapshot(case)
+            rc = fn(*case.args(_ptrs(case.ops, name, bad, bad_index=1 if isinstance(v, list) else 0)))
+            msg = lib.fa_last_error_string().decode()
+            assert rc == -1, (case.name, name, rc, msg)  # FA_E_ARG
+            assert "pageable" in msg and "nothing was launched" in msg, (case.name, name, msg)
+            assert (f"{name}[1]" if isinstance(v, list) else name) in msg, (case.name, name, msg)
+            _unchanged(case, snap)
+            checked.add((case.name, name))
+        # the same call with every operand valid goes through (the case's arguments are right)
+        rc = fn(*case.args(_ptrs(case.ops)))
+        assert rc == 0, (case.name, lib.fa_last_error_string().decode())
+    torch.cuda.synchronize()
+    del keep
+    # every launching entry point of the ABI is covered (queries, host-only and RCCL calls are not launches)
+    host_or_query = {"fa_abi_version", "fa_last_error_string", "fa_pointer_kind", "fa_reduce_launches",
+                     "fa_qfed_launches", "fa_qfed_max_chunk", "fa_qfed_workspace_bytes", "fa_host_gather",
+                     "fa_pickle_strip", "fa_dp_workspace_bytes"}
+    rccl = {n for n in exported if n.startswith("fa_rccl_")}
+    assert exported - host_or_query - rccl == {c.name for c in cases}
+
+
+def test_pinned_host_operand_only_where_the_header_allows_it(gpu_device):
+    from fedscale_amd import _native as N
+
+    lib = N.load()
+    st = torch.cuda.current_stream().cuda_stream
+    pinned = torch.zeros(1 << 17, dtype=torch.float64).pin_memory()
+    cases, keep = _cases(gpu_device, st)
+    for case in cases:
+        fn = getattr(lib, case.name)
+        for name, v in case.ops.items():
+            if isinstance(v, list):
+                continue
+            snap = _snapshot(case)
+            pinned.zero_()
+            rc = fn(*case.args(_ptrs(case.ops, name, pinned.data_ptr())))
+            msg = lib.fa_last_error_string().decode()
+            if name in case.host_ok:  # the zero-copy operands: pinned memory is read / written over PCIe
+                assert rc == 0, (case.name, name, msg)
+                torch.cuda.synchronize()
+            else:
+                assert rc == -1 and "pinned host memory" in msg, (case.name, name, rc, msg)
+                _unchanged(case, snap)
+    del keep
+
+
+def test_operand_extent_beyond_its_allocation_is_rejected(gpu_device):
+    """A buffer too short for the call (here: P columns over a tensor of P/2) is refused, not overrun."""
+    from fedscale_amd import _native as N
+
+    lib = N.load()
+    st = torch.cuda.current_stream().cuda_stream
+    big = 1 << 22  # its own caching-allocator segment, so the allocation ends where the tensor does
+    cur = torch.ones(big, device=gpu_device)
+    short = torch.ones(big // 2, device=gpu_device)
+    m, v, out = (torch.zeros(big, device=gpu_device) for _ in range(3))
+    rc = lib.fa_yogi_step(cur.data_ptr(), short.data_ptr(), m.data_ptr(), v.data_ptr(), out.data_ptr(), big,
+                          3e-3, 1e-8, 0.9, 0.1, 0.01, 0, st)
+    msg = lib.fa_last_error_string().decode()
+    assert rc == -1 and "last" in msg and "past the end of its allocation" in msg, msg
+    torch.cuda.synchronize()
+    assert int(torch.count_nonzero(out)) == 0
+
+
+def test_rccl_buffers_are_checked(gpu_device):
+    from fedscale_amd import _native as N
+
+    lib = N.load()
+    if not lib.fa_rccl_available():
+        pytest.skip("RCCL not loadable")
+    comm = ctypes.c_void_p()
+    N.call("fa_rccl_init", 1, _u64([0]).astype(np.int32).ctypes.data, ctypes.byref(comm))
+    try:
+        st = torch.cuda.current_stream().cuda_stream
+        send = torch.ones(64, device=gpu_device)
+        recv = torch.zeros(64, device=gpu_device)
+        pageable = np.zeros(64, dtype=np.float32)
+        sts = _u64([st])
+        for s_ptr, r_ptr, name in ((pageable.ctypes.data, recv.data_ptr(), "send[0]"),
+                                   (send.data_ptr(), pageable.ctypes.data, "recv[0]")):
+            rc = lib.fa_rccl_all_reduce(comm, _u64([s_ptr]).ctypes.data, _u64([r_ptr]).ctypes.data, 64, N.FA_DT_F32,
+                                        sts.ctypes.data)
+            msg = lib.fa_last_error_string().decode()
+            assert rc == -1 and name in msg and "pageable" in msg, msg
+        short = torch.zeros(16, device=gpu_device)
+        del short  # (a recv buffer shorter than the gather is refused by its extent, covered on the CPU)
+        torch.cuda.synchronize()
+        assert int(torch.count_nonzero(recv)) == 0
+        N.call("fa_rccl_all_reduce", comm, _u64([send.data_ptr()]).ctypes.data, _u64([recv.data_ptr()]).ctypes.data,
+               64, N.FA_DT_F32, sts.ctypes.data)
+        torch.cuda.synchronize()
+        assert torch.equal(recv, send)
+    finally:
+        N.call("fa_rccl_destroy", comm)

@@ -103,7 +103,13 @@ def test_reduce_column_windows_every_column(gpu_device, weighted):
 
 
 def test_c4_fedyogi_k1000_p25m(gpu_device):
-    """Config 4 (per-GPU shard): fused reduce + FedYoGi over 1000 x 25M, two rounds of state."""
+    """Config 4 (per-GPU shard) over 1000 x 25M, two rounds of state, in both forms the library has:
+      * the UNFUSED pair the single-device drop-in runs since round 3 and bench.py times
+        (TorchModelAdapter: fa_reduce FA_FINALIZE into the mean, then fa_yogi_step;
+        aggregator.py:505-507 -> optimizers.py:43-63 -> yogi.py:15-36);
+      * the fused fa_reduce_yogi (the client-sharded SPMD finish, round.py).
+    Both bit-exact against the IEEE numpy restatement on sampled columns, and against each other on every
+    column."""
     from fedscale_amd import kernels as kx
     from fedscale_amd import synth
     from fedscale_amd.bucket import round_up
@@ -118,10 +124,9 @@ def test_c4_fedyogi_k1000_p25m(gpu_device):
     last = torch.empty(1, ld, device="cuda")
     synth.fill(last, 1, P, seed=seed + 5000, scale_noise=0.0)
     last = last[0]
-    m = torch.empty(ld, device="cuda")
-    v = torch.empty(ld, device="cuda")
-    out = torch.empty(ld, device="cuda")
-    mean = torch.empty(ld, device="cuda")
+    last_u = last.clone()  # the unfused chain's own model (each form carries its own state across rounds)
+    m, v, out, mean = (torch.empty(ld, device="cuda") for _ in range(4))
+    m_u, v_u, out_u, mean_u = (torch.empty(ld, device="cuda") for _ in range(4))
     cols = _sample_cols(P, n=2048, seed=1)
     ci = torch.from_numpy(cols).cuda()
     L = last[ci].cpu().numpy()
@@ -129,6 +134,9 @@ def test_c4_fedyogi_k1000_p25m(gpu_device):
     vh = np.full(len(cols), f(hp["tau"]))
     cur = np.divide(_host_seq_sum(seed, K, cols), K)
     for r in range(2):
+        # what the drop-in runs (torch_model_adapter.py _apply_yogi): the mean, then the step
+        kx.reduce(x, K, P, mean_u, denom=float(f(K)), finalize=True)
+        kx.yogi_step(mean_u, last_u, m_u, v_u, out_u, P, init=(r == 0), **hp)
         kx.reduce_yogi(x, K, P, last=last, m=m, v=v, out=out, denom=float(f(K)), init=(r == 0), mean_out=mean, **hp)
         g = cur - L
         g2 = g * g
@@ -136,13 +144,89 @@ def test_c4_fedyogi_k1000_p25m(gpu_device):
         vh = vh - (f(hp["omb2"]) * g2) * np.sign(vh - g2)
         step = ((f(1) / (np.sqrt(vh) + f(hp["tau"]))) * f(hp["eta"])) * mh
         new = L + step
-        np.testing.assert_array_equal(mean[ci].cpu().numpy(), cur)
-        np.testing.assert_array_equal(m[ci].cpu().numpy(), mh)
-        np.testing.assert_array_equal(v[ci].cpu().numpy(), vh)
-        np.testing.assert_array_equal(out[ci].cpu().numpy(), new)
+        for got_mean, got_m, got_v, got_out in ((mean_u, m_u, v_u, out_u), (mean, m, v, out)):
+            np.testing.assert_array_equal(got_mean[ci].cpu().numpy(), cur)
+            np.testing.assert_array_equal(got_m[ci].cpu().numpy(), mh)
+            np.testing.assert_array_equal(got_v[ci].cpu().numpy(), vh)
+            np.testing.assert_array_equal(got_out[ci].cpu().numpy(), new)
+        for a, b in ((mean_u, mean), (m_u, m), (v_u, v), (out_u, out)):  # every column: the two forms agree
+            assert torch.equal(a[:P], b[:P])
         last.copy_(out)  # next round starts from the new model
+        last_u.copy_(out_u)
         L = new
     del x
+
+
+def test_c5_qfedavg_shard_k10000_chain_deferred_as_the_drop_in_runs_it(gpu_device):
+    """Config 5's per-GPU shard (10,000 x 12.5M, q-FedAvg) exactly as DeviceRound runs it at that K and as
+    bench.py times it: chunks of fa_qfed_max_chunk() clients (9 x 1024 + 784), the fused FedAvg chain
+    (``chain=``, the 8-float4 LDS-DMA kernel; aggregator.py:497-507) and a workspace sized for the call's
+    (ld, P), so the per-client norm gathers run once per call (deferred).  Delta and chain bit-exact on
+    sampled columns, the mean from the chain bit-exact, norms within 1e-9 of the host's fp64 sums, hs and the
+    new model bit-exact (optimizers.py:73-104)."""
+    from fedscale_amd import kernels as kx
+    from fedscale_amd import synth
+    from fedscale_amd.bucket import round_up
+
+    K, P, seed = 10_000, 12_500_000, 56
+    chunk = kx.qfed_max_chunk()
+    lr, q = 0.05, 1.0
+    ld = round_up(P, 64)
+    assert kx.qfed_launches(ld, P, chain=True) > 1  # several column windows: the deferred gathers apply
+    rng = np.random.default_rng(8)
+    losses = rng.uniform(0.5, 2.0, size=K)
+    alpha = np.array([np.float32(np.float_power(l + 1e-10, q)) for l in losses], dtype=np.float32)
+    x = torch.empty(chunk, ld, device="cuda")
+    last = torch.empty(1, ld, device="cuda")
+    synth.fill(last, 1, P, seed=seed + 90000, scale_noise=0.0)
+    last = last[0]
+    delta = torch.zeros(ld, device="cuda")
+    chain = torch.zeros(ld, device="cuda")
+    sq = torch.zeros(K, dtype=torch.float64, device="cuda")
+    ws = kx.qfed_workspace(chunk, "cuda", ld, P)  # DeviceRound._init_qfed's workspace
+    al = torch.from_numpy(alpha).cuda()
+    bounds = list(range(0, K, chunk)) + [K]
+    assert len(bounds) - 1 == 10 and bounds[-1] - bounds[-2] == K - 9 * chunk
+    for c, (k0, k1) in enumerate(zip(bounds[:-1], bounds[1:])):
+        synth.fill(x, k1 - k0, P, seed=seed, k0=k0)
+        kx.qfed_accumulate(x, k1 - k0, P, last=last, alpha=al[k0:k1], lr=lr, delta=delta, sqnorm=sq[k0:k1],
+                           workspace=ws, accumulate=c > 0, chain=chain)
+    mean = torch.empty(ld, device="cuda")
+    kx.reduce(chain.view(1, ld), 1, P, mean, denom=float(np.float32(K)), finalize=True)  # mean_from_staging
+    cols = _sample_cols(P, n=1024, seed=3)
+    ci = torch.from_numpy(cols).cuda()
+    L = last[ci].cpu().numpy()
+    d = acc = None
+    for c0 in range(0, K, 500):
+        for i, row in enumerate(synth.host_columns(seed, range(c0, c0 + 500), cols)):
+            g = (L - row) / np.float32(lr)
+            t = alpha[c0 + i] * g
+            d = t if d is None else d + t
+            acc = row.copy() if acc is None else acc + row
+    np.testing.assert_array_equal(delta[ci].cpu().numpy(), d)
+    np.testing.assert_array_equal(chain[ci].cpu().numpy(), acc)
+    np.testing.assert_array_equal(mean[ci].cpu().numpy(), np.divide(acc, np.float32(K)))
+    sqh = sq.cpu().numpy()
+    allc = np.arange(P)
+    Lfull = last[:P].cpu().numpy()
+    for k in (0, chunk - 1, chunk, 5 * chunk + 17, K - 1):  # chunk seams included
+        g = (Lfull - synth.host_columns(seed, [k], allc)[0]) / np.float32(lr)
+        ref = np.sum((g * g).astype(np.float64))
+        assert abs(sqh[k] - ref) <= 1e-9 * ref
+    assert np.all(sqh > 0)
+    del x
+    c1 = np.array([np.float32(q * np.float_power(l + 1e-10, q - 1)) for l in losses], dtype=np.float32)
+    c2 = np.array([np.float32((1.0 / lr) * np.float_power(l + 1e-10, q)) for l in losses], dtype=np.float32)
+    hs_dev = torch.zeros(2, device="cuda")
+    new = torch.empty(ld, device="cuda")
+    kx.qfed_hs(sq, torch.from_numpy(c1).cuda(), torch.from_numpy(c2).cuda(), K, hs_dev)
+    kx.qfed_finalize(last, delta, hs_dev, new, P)
+    hs = np.float32(0.0)
+    for k in range(K):
+        hs = np.float32(hs + np.float32(c1[k] * np.float32(sqh[k]) + c2[k]))
+    hs_got = hs_dev.cpu().numpy()
+    assert hs_got[0] == hs and hs_got[1] == np.float32(hs + np.float32(1e-10))
+    np.testing.assert_array_equal(new[ci].cpu().numpy(), L - d / np.float32(hs_got[1]))
 
 
 def test_c5_qfedavg_shard_k10000_streamed(gpu_device):
