@@ -305,23 +305,35 @@ def pcie_inclusive_leg(dev, seed: int, K: int = 64, rounds: int = 6) -> dict:
         payloads.append(pickle.dumps({"client_id": i, "moving_loss": 1.0, "trained_size": 200, "success": True,
                                       "utility": 1.0, "update_weight": up, "wall_duration": 0}))
         del up
-    ts = []
+    ts, t_in, t_fin, t_eg = [], [], [], []
     for r in range(rounds + 1):
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         agg.start_round(K)
-        for k in range(K):
+        for k in range(K - 1):
             agg.on_result(agg.deserialize_response(payloads[k % 8]))
+        t1 = time.perf_counter()
+        agg.on_result(agg.deserialize_response(payloads[(K - 1) % 8]))  # the K-th: its H2D, then the reduce
+        torch.cuda.synchronize(dev)
+        t2 = time.perf_counter()
         adapter.get_weights()
+        t3 = time.perf_counter()
         if r:
-            ts.append(time.perf_counter() - t0)
+            ts.append(t3 - t0)
+            t_in.append(t1 - t0)
+            t_fin.append(t2 - t1)
+            t_eg.append(t3 - t2)
     s, smin = float(np.median(ts)), float(np.min(ts))
+    tin = float(np.median(t_in))
     P = adapter.layout.P_full
     del agg, adapter, payloads
     torch.cuda.empty_cache()
     return {"clients": K, "params": P, "round_ms": s * 1e3, "round_ms_min": smin * 1e3,
             "rounds_ms": [t * 1e3 for t in ts], "client_updates_per_s": K / s, "client_updates_per_s_best": K / smin,
             "host_to_device_GBps": 4 * K * P / s / 1e9, "host_to_device_GBps_best": 4 * K * P / smin / 1e9,
+            "phases_ms": {"ingress_first_K_minus_1": tin * 1e3, "last_upload_and_reduce": float(np.median(t_fin)) * 1e3,
+                          "egress_get_weights": float(np.median(t_eg)) * 1e3},
+            "ingress_GBps": 4 * (K - 1) * P / tin / 1e9,
             "note": "from pickled executor payloads: zero-copy deserialize_response, pinned gather + H2D, reduce, "
                     "get_weights() D2H; median and min of %d rounds after one warm-up round; bound by one PCIe "
                     "link, never `value`" % rounds}

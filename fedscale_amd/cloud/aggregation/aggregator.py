@@ -75,9 +75,12 @@ class DeviceAggregatorMixin:
     device_egress_past_versions = 8
     #: GPU ordinals to shard the model over inside this process (None: FEDAGG_DEVICES, else one GPU)
     device_shards = None
-    #: bind the main thread (which stages every upload into pinned memory) to the CPUs of the GPU's NUMA node,
-    #: so the staging lands next to the GPU's PCIe link (fedscale_amd/hostnuma.py); single-GPU adapters only
-    device_numa_bind = True
+    #: opt-in: bind the main thread (which stages every upload into pinned memory) to the CPUs of the GPU's NUMA
+    #: node, so the staging lands next to the GPU's PCIe link (fedscale_amd/hostnuma.py; single-GPU adapters).  Off
+    #: by default: the affinity is process-wide in effect (every thread the main thread starts later inherits it:
+    #: torch's intra-op pool, gRPC work), for ~7 us on config 1's round (profiles/r03_numa_probe.log).  When on,
+    #: torch's intra-op thread count is lowered to the node's CPUs and the binding is logged
+    device_numa_bind = False
 
     _device_round = None
 
@@ -129,7 +132,7 @@ class DeviceAggregatorMixin:
             if self.device_numa_bind:
                 from ...hostnuma import bind_to_gpu
 
-                bind_to_gpu(getattr(self.model_wrapper, "device", dev))
+                bind_to_gpu(getattr(self.model_wrapper, "device", dev), match_torch_threads=True, log=True)
 
     def _wrapper(self) -> TorchModelAdapter:
         w = self.model_wrapper

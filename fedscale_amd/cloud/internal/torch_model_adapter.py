@@ -89,7 +89,7 @@ class _HostBuf:
     """Pinned host buffers for one model version (fp32 bucket ``f``, side table ``s``) with their state_dict
     views, made once: buffers are pooled across versions, so egress clones from ready-made views."""
 
-    __slots__ = ("f", "s", "views", "np_views")
+    __slots__ = ("f", "s", "views", "np_views", "ev")
 
     def __init__(self, layout: BucketLayout):
         # round_up(P, 4) floats: fa_reduce_mirror writes whole float4 columns into ``f``
@@ -97,11 +97,14 @@ class _HostBuf:
         self.s = torch.empty(max(1, layout.Q), dtype=torch.int64)
         self.views = layout.unpack(self.f, self.s)
         self.np_views = [v.numpy() for v in self.views]
+        # recorded after the kernel that writes this buffer (fa_reduce_mirror); re-recorded only while the buffer
+        # is out of the pool, i.e. while no reader can be waiting on it
+        self.ev = torch.cuda.Event()
 
 
 class _HostSnapshot:
     """One model version's host copy (a ``_HostBuf``) and its reader count.  ``pending``: the round's kernel
-    writes the buffer itself (fa_reduce_mirror) and the first reader waits for the model's ready event."""
+    writes the buffer itself (fa_reduce_mirror) and the first reader waits for that kernel (``buf.ev``)."""
 
     __slots__ = ("version", "buf", "readers", "pending")
 
@@ -192,6 +195,7 @@ class TorchModelAdapter(ModelAdapterBase):
             self._cur = 1 - self._cur
             self._version += 1
             if host is not None:
+                host.ev.record(self._ready_stream)  # this version's kernel: what its readers wait for
                 old, self._snap = self._snap, _HostSnapshot(self._version, host, pending=True)
                 if old is not None and old.readers == 0:
                     self._snap_pool.append(old.buf)
@@ -277,7 +281,21 @@ class TorchModelAdapter(ModelAdapterBase):
         with self._egress_lock:
             snap = self._snap
             if snap is not None and snap.pending and snap.version == self._version:
-                self._ready.synchronize()  # the round's kernel wrote this snapshot (fa_reduce_mirror)
+                snap.readers += 1  # held: it cannot return to the pool while this thread waits
+                wait = snap.buf.ev
+            else:
+                wait = None
+        if wait is not None:
+            # the kernel of THIS version wrote the snapshot (fa_reduce_mirror): wait for it alone, outside the
+            # lock, so neither the next round's kernels nor the other egress readers hold this thread up
+            wait.synchronize()
+            with self._egress_lock:
+                snap.pending = False
+            return snap
+        with self._egress_lock:
+            snap = self._snap
+            if snap is not None and snap.pending and snap.version == self._version:
+                snap.buf.ev.synchronize()  # (another thread published a pending version meanwhile)
                 snap.pending = False
             if snap is None or snap.version != self._version:
                 buf = self._snap_pool.pop() if self._snap_pool else _HostBuf(self.layout)

@@ -37,6 +37,14 @@
 // 3: fa_qfed_accumulate takes the workspace's size, fa_qfed_workspace_bytes the call's (ld, P) (deferred gathers)
 #define FA_ABI_VERSION 3
 
+// FA_TUNING 1 (tools/build_*variants.sh) compiles the measured-and-rejected alternatives kept for re-measurement:
+// the second q-FedAvg design (k_qfed_accum2), the level cascade of fixed variants, the multi-round capped grid,
+// raw-buffer / XCD-remapped / pipelined k_reduce loads and the fixed-variant builds (FA_RED_V).  The default
+// library holds only what the drop-in launches.
+#ifndef FA_TUNING
+#define FA_TUNING 0
+#endif
+
 typedef float f4 __attribute__((ext_vector_type(4)));
 
 // ------------------------------------------------------------------------------------------------
@@ -91,6 +99,9 @@ __device__ __forceinline__ f4 ldnt(const f4* p) {
 
 #ifndef FA_RED_BUF
 #define FA_RED_BUF 0  // tuning: 1 = k_reduce reads client rows with raw buffer loads of cache policy FA_RED_AUX
+#endif
+#if !FA_TUNING && (FA_RED_BUF || !FA_RED_NT)
+#error "FA_RED_BUF / FA_RED_NT=0 are tuning knobs: build with -DFA_TUNING=1"
 #endif
 #ifndef FA_RED_AUX
 #define FA_RED_AUX 2  // buffer-load cache policy bits (gfx950: 1 sc0, 2 nt, 16 sc1)
@@ -169,6 +180,9 @@ struct RedArgs {
 #endif
 #ifndef FA_PIPE
 #define FA_PIPE 0  // 1: every variant software-pipelines its client groups (tuning builds)
+#endif
+#if !FA_TUNING && (FA_XCD_REMAP || FA_PIPE || FA_RED_WAVES != 4)
+#error "FA_XCD_REMAP / FA_PIPE / FA_RED_WAVES are tuning knobs: build with -DFA_TUNING=1"
 #endif
 // One tile: the workgroup's FA_RED_WAVES waves each own 64*sw float4 columns (sw <= V strips, a run-time
 // width; FULL: sw == V, the compile-time width) and walk all K clients.
@@ -325,6 +339,9 @@ __global__ __launch_bounds__(64 * FA_RED_WAVES) void k_reduce(RedArgs r) {
 // (occupancy x CUs, queried at run time), the next narrower variant the same on what is left, the
 // narrowest the remainder.  Every column is still reduced by exactly one thread in arrival order, so no
 // plan changes a bit of the result.
+#if defined(FA_RED_V) && !FA_TUNING
+#error "FA_RED_V (a single fixed variant) is a tuning build: add -DFA_TUNING=1"
+#endif
 #ifdef FA_RED_V  // tuning build: a single fixed variant
 #define FA_LEVELS 1
 #define FA_L0_V FA_RED_V
@@ -357,6 +374,18 @@ static int cu_count() {
   return cus;
 }
 
+// fa_reduce_launches() runs the launch plan with g_plan_count set: every k_reduce launch site then counts
+// instead of launching, so the plan has one source of truth.
+static thread_local int64_t* g_plan_count = nullptr;
+#define FA_RED_LAUNCH(kern, grid, block, st, args)         \
+  do {                                                     \
+    if (g_plan_count)                                      \
+      ++*g_plan_count;                                     \
+    else                                                   \
+      hipLaunchKernelGGL(kern, grid, block, 0, st, args);  \
+  } while (0)
+
+#if FA_TUNING
 template <int V, int U, int EPI, bool W>
 static int resident_blocks() {
   static int cache[64];  // per device ordinal: occupancy x CU count (idempotent, benign race)
@@ -370,17 +399,6 @@ static int resident_blocks() {
   cache[dev] = per_cu * cu_count();
   return cache[dev];
 }
-
-// fa_reduce_launches() runs the launch plan with g_plan_count set: every k_reduce launch site then counts
-// instead of launching, so the plan has one source of truth.
-static thread_local int64_t* g_plan_count = nullptr;
-#define FA_RED_LAUNCH(kern, grid, block, st, args)         \
-  do {                                                     \
-    if (g_plan_count)                                      \
-      ++*g_plan_count;                                     \
-    else                                                   \
-      hipLaunchKernelGGL(kern, grid, block, 0, st, args);  \
-  } while (0)
 
 // launch variant (V, U) over float4 columns [col, col_end); `full_waves_only` keeps only whole waves of
 // workgroups (a last partial wave is kept when it would still occupy >= 90 % of the resident slots: a
@@ -413,6 +431,7 @@ static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_w
   const int64_t end = col + nblk * span;
   return (full_waves_only && end < col_end) ? end : col_end;
 }
+#endif  // FA_TUNING (the level cascade)
 
 // Balanced launches (run-time tile width sw strips per wave, sw <= the variant's V; every workgroup gets
 // the same number of equally wide tiles, the last tile ragged).  With S strips of 64 float4 columns:
@@ -444,6 +463,9 @@ static int64_t launch_level(RedArgs r, int64_t col, int64_t col_end, bool full_w
 #define FA_CAP_SW_MAX 32  // widest tile (strips per wave) of the multi-round capped plan (tuning knob, 8..32)
 #endif
 static_assert(FA_CAP_SW_MAX >= 8 && FA_CAP_SW_MAX <= 32, "FA_CAP_SW_MAX: 8..32");
+#ifndef FA_WINDOWS
+#define FA_WINDOWS 1
+#endif
 template <int V, int U, int EPI, bool W>
 static void launch_balanced(RedArgs r, int64_t sw, int64_t rounds, hipStream_t st) {
   const int64_t S = (r.P4 + 63) / 64;
@@ -452,12 +474,17 @@ static void launch_balanced(RedArgs r, int64_t sw, int64_t rounds, hipStream_t s
   r.ntiles = (S + (int64_t)FA_RED_WAVES * sw - 1) / ((int64_t)FA_RED_WAVES * sw);
   const int64_t grid = (r.ntiles + rounds - 1) / rounds;
   const dim3 blk(64 * FA_RED_WAVES);
-  if (grid < r.ntiles) {
+#if FA_TUNING || !FA_WINDOWS || FA_CAP_SW_MAX != 32
+  if (grid < r.ntiles) {  // several rounds of the capped grid in one launch (the window plan replaces it)
     if (sw == V)
       FA_RED_LAUNCH((k_reduce<V, U, EPI, W, true, true>), dim3((unsigned)grid), blk, st, r);
     else
       FA_RED_LAUNCH((k_reduce<V, U, EPI, W, true, false>), dim3((unsigned)grid), blk, st, r);
-  } else if (sw == V) {
+    return;
+  }
+#endif
+  (void)grid;
+  if (sw == V) {
     FA_RED_LAUNCH((k_reduce<V, U, EPI, W, false, true>), dim3((unsigned)r.ntiles), blk, st, r);
   } else {
     FA_RED_LAUNCH((k_reduce<V, U, EPI, W, false, false>), dim3((unsigned)r.ntiles), blk, st, r);
@@ -494,9 +521,6 @@ static void launch_window(RedArgs r, int64_t s0, int64_t ns, int64_t cap, hipStr
 // re-aligns them.  Measured interleaved on three boxes (tools/window_probe.py, profiles/r02_window_probe.log):
 // 1000 x 25 M 7.07-7.09 -> 7.15-7.16 TB/s, 1000 x 12.5 M +0.6 %; the bits are the same (columns are
 // independent).
-#ifndef FA_WINDOWS
-#define FA_WINDOWS 1
-#endif
 // Short, narrow rounds (config 2: 100 x 1 M, 400 MB per round): one launch, one workgroup per tile of 4
 // waves x 4 float4 per lane, the client groups software-pipelined (two register buffers of 4 clients: the
 // next group's 16 KiB per wave is in flight while the current one is added, so 32 KiB per wave is
@@ -515,74 +539,76 @@ static void launch_short(RedArgs r, hipStream_t st) {
   FA_RED_LAUNCH((k_reduce<4, 4, EPI, W, false, true, true>), dim3((unsigned)r.ntiles), dim3(64 * FA_RED_WAVES), st, r);
 }
 template <int EPI, bool W>
-static void launch_plan(const RedArgs& r, hipStream_t st) {
-  int64_t col = 0;
-#if FA_LEVELS == 1
+static int launch_plan(const RedArgs& r, hipStream_t st) {
+#if FA_LEVELS == 1  // tuning build: one fixed variant (FA_RED_V / FA_RED_U), optionally on a fixed grid cap
 #if defined(FA_RED_GRID) && FA_RED_GRID > 0
-  launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, false, FA_RED_GRID, st);  // tuning: fixed cap
+  launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, 0, r.P4, false, FA_RED_GRID, st);
 #else
-  launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, false, 0, st);
+  launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, 0, r.P4, false, 0, st);
 #endif
+  return FA_OK;
 #else
-  const int64_t cap = (int64_t)cu_count() * FA_GRID_CAP_PCT / 100;
-  const int64_t span0 = 64LL * FA_RED_WAVES * FA_L0_V;
-  const int64_t tiles0 = (r.P4 + span0 - 1) / span0;
+  const int64_t cus = cu_count();
+  if (cus <= 0) return fail(FA_E_HIP, "k_reduce launch plan: no CU count for device %d", fa_scope_device());
+  const int64_t cap = cus * FA_GRID_CAP_PCT / 100;
 #if FA_BAL_GRID > 0
-  if (cap > 0) {
+  {
     const int64_t S = (r.P4 + 63) / 64;
-    const int64_t g1 = r.K < FA_BAL_SHORT_K ? (int64_t)cu_count() : cap;  // short rounds: one round, all CUs
+    const int64_t g1 = r.K < FA_BAL_SHORT_K ? cus : cap;  // short rounds: one round, all CUs
     const int64_t sw1 = (S + (int64_t)FA_RED_WAVES * g1 - 1) / ((int64_t)FA_RED_WAVES * g1);
     if (sw1 > 32) {  // R rounds of the capped grid, tiles at most FA_CAP_SW_MAX strips wide
       const int64_t per_round = (int64_t)FA_RED_WAVES * FA_CAP_SW_MAX * cap;
       const int64_t R = (S + per_round - 1) / per_round;
-      if (FA_WINDOWS && FA_CAP_SW_MAX == 32) {
+      if (FA_WINDOWS && FA_CAP_SW_MAX == 32) {  // ... as R launches over column windows, one round each
         const int64_t Sw = (S + R - 1) / R;
         for (int64_t s0 = 0; s0 < S; s0 += Sw) launch_window<EPI, W>(r, s0, S - s0 < Sw ? S - s0 : Sw, cap, st);
-        return;
+        return FA_OK;
       }
       const int64_t sw = (S + (int64_t)FA_RED_WAVES * R * cap - 1) / ((int64_t)FA_RED_WAVES * R * cap);
       if (sw > 16)
         launch_balanced<32, 1, EPI, W>(r, sw, R, st);
       else
         launch_balanced<16, 2, EPI, W>(r, sw, R, st);
-      return;
+      return FA_OK;
     }
     if (sw1 >= 8) {  // one round of wide tiles on (about) the capped grid
       if (sw1 > 16)
         launch_balanced<32, 1, EPI, W>(r, sw1, 1, st);
       else
         launch_balanced<16, 2, EPI, W>(r, sw1, 1, st);
-      return;
+      return FA_OK;
     }
     // narrow tiles: one round on more workgroups, unless the round is short
-    const int64_t gb = (int64_t)cu_count() * FA_BAL_GRID / 256;
+    const int64_t gb = cus * FA_BAL_GRID / 256;
     const int64_t swb = (S + (int64_t)FA_RED_WAVES * gb - 1) / ((int64_t)FA_RED_WAVES * gb);
     if (swb >= FA_BAL_MIN_SW && (int64_t)r.K * swb >= FA_BAL_MIN_WORK) {
       if (swb > 8)
         launch_balanced<16, 2, EPI, W>(r, swb, 1, st);
       else
         launch_balanced<8, 4, EPI, W>(r, swb, 1, st);
-      return;
+      return FA_OK;
     }
   }
 #endif
 #if FA_SHORT_PIPE
-  if (cap > 0) {  // narrow, short round (K x sw < FA_BAL_MIN_WORK, e.g. config 2's 100 x 1 M)
-    launch_short<EPI, W>(r, st);
-    return;
-  }
-#endif
-  if (cap > 0 && tiles0 * 20 >= cap * 17) {  // enough widest tiles to keep ~cap workgroups busy
+  launch_short<EPI, W>(r, st);  // narrow, short round (K x sw < FA_BAL_MIN_WORK, e.g. config 2's 100 x 1 M)
+  return FA_OK;
+#elif FA_TUNING
+  // rounds 1-2's level cascade (tuning builds with FA_SHORT_PIPE=0 or FA_BAL_GRID=0)
+  const int64_t span0 = 64LL * FA_RED_WAVES * FA_L0_V;
+  const int64_t tiles0 = (r.P4 + span0 - 1) / span0;
+  if (tiles0 * 20 >= cap * 17) {  // enough widest tiles to keep ~cap workgroups busy
     launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, 0, r.P4, false, cap, st);
-    return;
+    return FA_OK;
   }
-#ifndef FA_YOGI_SKIP_L0
-#define FA_YOGI_SKIP_L0 0
-#endif
-  if (!(EPI == EPI_YOGI && FA_YOGI_SKIP_L0)) col = launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, col, r.P4, true, 0, st);
+  int64_t col = launch_level<FA_L0_V, FA_L0_U, EPI, W>(r, 0, r.P4, true, 0, st);
   if (col < r.P4) col = launch_level<FA_L1_V, FA_L1_U, EPI, W>(r, col, r.P4, true, 0, st);
   if (col < r.P4) col = launch_level<FA_L2_V, FA_L2_U, EPI, W>(r, col, r.P4, true, 0, st);
   if (col < r.P4) launch_level<FA_L3_V, FA_L3_U, EPI, W>(r, col, r.P4, false, 0, st);
+  return FA_OK;
+#else
+#error "FA_SHORT_PIPE=0 / FA_BAL_GRID=0 fall back to the level cascade: a tuning build (-DFA_TUNING=1)"
+#endif
 #endif
 }
 
@@ -590,10 +616,8 @@ template <int EPI>
 static int launch_reduce(const RedArgs& r, hipStream_t st, const char* what) {
   if (r.P4 <= 0) return FA_OK;
   if (r.P4 / (64 * FA_RED_WAVES) > 0x7fffffffLL) return fail(FA_E_RANGE, "%s: P too large", what);
-  if (r.a)
-    launch_plan<EPI, true>(r, st);
-  else
-    launch_plan<EPI, false>(r, st);
+  const int e = r.a ? launch_plan<EPI, true>(r, st) : launch_plan<EPI, false>(r, st);
+  if (e) return e;
   return check_launch(what);
 }
 
@@ -605,12 +629,9 @@ extern "C" int64_t fa_reduce_launches(int32_t K, int64_t P, int32_t weighted) {
   r.K = K;
   int64_t n = 0;
   g_plan_count = &n;
-  if (weighted)
-    launch_plan<EPI_MEAN, true>(r, nullptr);
-  else
-    launch_plan<EPI_MEAN, false>(r, nullptr);
+  const int e = weighted ? launch_plan<EPI_MEAN, true>(r, nullptr) : launch_plan<EPI_MEAN, false>(r, nullptr);
   g_plan_count = nullptr;
-  return n;
+  return e ? e : n;
 }
 
 static int check_reduce_args(const char* what, const float* x, int64_t ld, int32_t K, int64_t P,
@@ -759,6 +780,12 @@ static_assert(QF_G == 8 || QF_G == 4, "QF_G must be 4 or 8");
 #ifndef QF_GRID
 #define QF_GRID 256  // one workgroup per CU at 1 wave/SIMD (profiles/r01_tune_qfed.log)
 #endif
+#ifndef QF_CHAIN_GRID
+#define QF_CHAIN_GRID QF_GRID  // the chain launches' grid (their 8-float4 tiles leave room for 2 workgroups per CU)
+#endif
+static_assert(QF_GRID % 16 == 0 && QF_CHAIN_GRID % 16 == 0, "the norm gathers sum the grid's rows in 16 segments");
+// workgroups of a k_qfed_accum launch (fixed per kind, so the fp64 norm order is the same on every run and device)
+static inline int qf_grid(bool chain) { return chain ? QF_CHAIN_GRID : QF_GRID; }
 
 #ifndef QF_BALANCE
 #define QF_BALANCE 1  // 0: always full-width tiles (plain grid-stride)
@@ -1115,6 +1142,7 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
     q.part[(int64_t)blockIdx.x * q.K + k] = ((sq[0][k] + sq[1][k]) + sq[2][k]) + sq[3][k];
 }
 
+#if FA_TUNING
 // ------------------------------------------------------------------------------------------------
 // q-FedAvg phase 1, second design (QF_KERNEL / QF_CHAIN_KERNEL 2; measured slower, built off): 2 waves per SIMD
 // ------------------------------------------------------------------------------------------------
@@ -1305,6 +1333,7 @@ __global__ __launch_bounds__(256) void k_qfed_gather2b(const double* __restrict_
   sqnorm[k] += s;
 }
 static_assert(QF2_ROWS % QF2_SEG == 0, "gather segments must divide the partial rows");
+#endif  // FA_TUNING (k_qfed_accum2)
 
 #define QF_GATHER_SEG 16
 __global__ __launch_bounds__(256) void k_qfed_gather_seg(const double* __restrict__ part, int nrows, int K,
@@ -1318,7 +1347,8 @@ __global__ __launch_bounds__(256) void k_qfed_gather_seg(const double* __restric
   for (int r = 0; r < rps; ++r) s += p[(int64_t)r * K];
   seg[(int64_t)blockIdx.y * K + k] = s;
 }
-static_assert(QF_GRID % QF_GATHER_SEG == 0, "gather segments must divide the grid");
+static_assert(QF_GRID % QF_GATHER_SEG == 0 && QF_CHAIN_GRID % QF_GATHER_SEG == 0,
+              "gather segments must divide the grid");
 
 __global__ __launch_bounds__(256) void k_qfed_gather(const double* __restrict__ part, int nblk, int K,
                                                      double* sqnorm) {
@@ -1364,13 +1394,19 @@ extern "C" int fa_qfed_max_chunk(void) { return QF_MAXK; }
 static int64_t qfed_window(int64_t ld, int64_t P, bool chain);
 // one window's partials + segments (the per-window gathers), either kernel family
 static int64_t qfed_ws_one(int64_t k) {
-  const int64_t w1 = ((int64_t)QF_GRID + QF_GATHER_SEG) * k * 8, w2 = ((int64_t)QF2_ROWS + QF2_SEG) * k * 8;
+  const int64_t g = QF_GRID > QF_CHAIN_GRID ? QF_GRID : QF_CHAIN_GRID;
+  const int64_t w1 = (g + QF_GATHER_SEG) * k * 8;
+#if FA_TUNING  // (the workspace size is part of the ABI: tuning builds keep the default build's figure or more)
+  const int64_t w2 = ((int64_t)QF2_ROWS + QF2_SEG) * k * 8;
+#else
+  const int64_t w2 = (2048LL + 32) * k * 8;  // = k_qfed_accum2's at its defaults: callers' workspaces stay valid
+#endif
   return w1 > w2 ? w1 : w2;
 }
 // every window's partials + segments (deferred gathers) of a call at (K, ld, P), chain or not
 static int64_t qfed_ws_deferred(int64_t k, int64_t ld, int64_t P, bool chain) {
   const int64_t win = qfed_window(ld, P, chain), nwin = P > win ? (P + win - 1) / win : 1;
-  return nwin * ((int64_t)QF_GRID + QF_GATHER_SEG) * k * 8;
+  return nwin * ((int64_t)qf_grid(chain) + QF_GATHER_SEG) * k * 8;
 }
 extern "C" int64_t fa_qfed_workspace_bytes(int32_t K, int64_t ld, int64_t P) {
   const int64_t k = K > 0 ? K : 1;
@@ -1385,6 +1421,9 @@ extern "C" int64_t fa_qfed_workspace_bytes(int32_t K, int64_t ld, int64_t P) {
 
 #ifndef QF_CHAIN_KERNEL
 #define QF_CHAIN_KERNEL 1
+#endif
+#if !FA_TUNING && ((defined(QF_KERNEL) && QF_KERNEL != 1) || QF_CHAIN_KERNEL != 1)
+#error "QF_KERNEL / QF_CHAIN_KERNEL 2 (k_qfed_accum2) is a tuning build: add -DFA_TUNING=1"
 #endif
 #ifndef QF_DEFER_GATHER
 #define QF_DEFER_GATHER 1  // one gather pair per call over every window's partials (workspace permitting)
@@ -1425,7 +1464,7 @@ static int64_t qfed_window(int64_t ld, int64_t P, bool chain) {
   const bool wide = (int64_t)ld * 4 * QF_G <= QF_WIDE_BYTES;
   int64_t win = wide ? (P > 0 ? P : 1) : (1LL << 28);
   const int64_t qv = chain ? QF_CHAIN_V : QF_V, rounds = chain ? QF_CHAIN_WIN_ROUNDS : QF_WIN_ROUNDS;
-  const int64_t cols = rounds * QF_GRID * 4 * qv * 256;  // rounds of full-width tiles
+  const int64_t cols = rounds * qf_grid(chain) * 4 * qv * 256;  // rounds of full-width tiles
   if (cols > 0 && win > cols) win = cols;
   return win;
 }
@@ -1449,7 +1488,8 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
   const int qv = chain ? QF_CHAIN_V : QF_V;
   const int64_t win = qfed_window(ld, P, chain != nullptr);
   const int64_t nwin = P > win ? (P + win - 1) / win : 1;
-  const int64_t per_win = (int64_t)QF_GRID * K;  // doubles of one window's partial rows
+  const int grid = qf_grid(chain != nullptr);
+  const int64_t per_win = (int64_t)grid * K;  // doubles of one window's partial rows
   // several windows and room for all their partials: one gather pair at the end (QF_DEFER_GATHER 0: off)
   const bool defer = QF_DEFER_GATHER && nwin > 1 && ws_bytes >= qfed_ws_deferred(K, ld, P, chain != nullptr);
   int64_t wi = 0;
@@ -1461,8 +1501,8 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
     qw.P4 = (pw + 3) / 4;
     {  // rounds r = tiles per workgroup at full width; then the narrowest tile that still needs r rounds
       const int64_t S = (qw.P4 + 63) / 64;
-      const int64_t r = (S + (int64_t)QF_GRID * 4 * qv - 1) / ((int64_t)QF_GRID * 4 * qv);
-      const int64_t strips = r > 0 ? (S + (int64_t)QF_GRID * r - 1) / ((int64_t)QF_GRID * r) : 1;
+      const int64_t r = (S + (int64_t)grid * 4 * qv - 1) / ((int64_t)grid * 4 * qv);
+      const int64_t strips = r > 0 ? (S + (int64_t)grid * r - 1) / ((int64_t)grid * r) : 1;
       qw.sw = (int)((strips + 3) / 4);
       if (qw.sw < 1) qw.sw = 1;
       if (qw.sw > qv || !QF_BALANCE) qw.sw = qv;
@@ -1470,20 +1510,20 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
     // chain launches: LDS-DMA prefetch (QF_CHAIN_GLDS slices) on QF_CHAIN_V-wide tiles; the plain kernel:
     // register loads on QF_V-wide tiles
     if (wide && chain)
-      hipLaunchKernelGGL((k_qfed_accum<true, true, QF_CHAIN_GLDS, QF_CHAIN_V>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<true, true, QF_CHAIN_GLDS, QF_CHAIN_V>), dim3(grid), dim3(256), 0, st, qw);
     else if (wide)
-      hipLaunchKernelGGL((k_qfed_accum<true, false, QF_PLAIN_GLDS, QF_V>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<true, false, QF_PLAIN_GLDS, QF_V>), dim3(grid), dim3(256), 0, st, qw);
     else if (chain)
-      hipLaunchKernelGGL((k_qfed_accum<false, true, QF_CHAIN_GLDS, QF_CHAIN_V>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<false, true, QF_CHAIN_GLDS, QF_CHAIN_V>), dim3(grid), dim3(256), 0, st, qw);
     else
-      hipLaunchKernelGGL((k_qfed_accum<false, false, QF_PLAIN_GLDS, QF_V>), dim3(QF_GRID), dim3(256), 0, st, qw);
+      hipLaunchKernelGGL((k_qfed_accum<false, false, QF_PLAIN_GLDS, QF_V>), dim3(grid), dim3(256), 0, st, qw);
     int e = check_launch("fa_qfed_accumulate");
     if (e) return e;
     if (!defer) {
-      // the QF_GRID partial rows, summed in a fixed two-level order (16 segments of QF_GRID/16 rows)
+      // the grid's partial rows, summed in a fixed two-level order (16 segments of grid/16 rows)
       double* seg = (double*)workspace + per_win;
       hipLaunchKernelGGL(k_qfed_gather_seg, dim3((K + 255) / 256, QF_GATHER_SEG), dim3(256), 0, st,
-                         (const double*)workspace, (int)QF_GRID, (int)K, seg);
+                         (const double*)workspace, grid, (int)K, seg);
       hipLaunchKernelGGL(k_qfed_gather, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)seg,
                          (int)QF_GATHER_SEG, (int)K, sqnorm);
       e = check_launch("fa_qfed_accumulate(gather)");
@@ -1495,7 +1535,7 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
     const int64_t nw = wi + 1;  // windows launched
     double* seg = (double*)workspace + nw * per_win;
     hipLaunchKernelGGL(k_qfed_gather_seg_win, dim3((K + 255) / 256, QF_GATHER_SEG, (unsigned)nw), dim3(256), 0, st,
-                       (const double*)workspace, (int)QF_GRID, (int)K, per_win, seg);
+                       (const double*)workspace, grid, (int)K, per_win, seg);
     hipLaunchKernelGGL(k_qfed_gather_win, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)seg, (int)K,
                        (int)nw, sqnorm);
     return check_launch("fa_qfed_accumulate(gather)");
@@ -1503,6 +1543,7 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
   return FA_OK;
 }
 
+#if FA_TUNING
 static int launch_qfed2(const float* x, int64_t ld, int32_t K, int64_t P, const float* last, const float* alpha,
                         float lr, int fast, float* delta, float* chain, double* sqnorm, void* workspace,
                         int32_t flags, hipStream_t st) {
@@ -1538,6 +1579,7 @@ static int launch_qfed2(const float* x, int64_t ld, int32_t K, int64_t P, const 
   }
   return FA_OK;
 }
+#endif  // FA_TUNING
 
 extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t P, const float* last,
                                   const float* alpha, float lr, float* delta, float* chain, double* sqnorm,
@@ -1562,8 +1604,10 @@ extern "C" int fa_qfed_accumulate(const float* x, int64_t ld, int32_t K, int64_t
   FA_OPERAND("workspace", workspace, (uint64_t)workspace_bytes);
   hipStream_t st = (hipStream_t)stream;
   const int fast = (lr >= 9.5367432e-07f && lr <= 1048576.f) ? 1 : 0;  // [2^-20, 2^20]
+#if FA_TUNING
   const int kern = chain ? QF_CHAIN_KERNEL : QF_KERNEL;
   if (kern == 2) return launch_qfed2(x, ld, K, P, last, alpha, lr, fast, delta, chain, sqnorm, workspace, flags, st);
+#endif
   return launch_qfed1(x, ld, K, P, last, alpha, lr, fast, delta, chain, sqnorm, workspace, workspace_bytes, flags,
                       st);
 }

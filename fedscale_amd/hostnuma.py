@@ -48,8 +48,10 @@ def node_cpus(node: int) -> Set[int]:
         return set()
 
 
-def bind_to_gpu(device) -> Optional[int]:
-    """Bind the calling thread to the CPUs of ``device``'s NUMA node; returns the node, or None if unchanged."""
+def bind_to_gpu(device, match_torch_threads: bool = False, log: bool = False) -> Optional[int]:
+    """Bind the calling thread to the CPUs of ``device``'s NUMA node; returns the node, or None if unchanged.
+    ``match_torch_threads``: lower torch's intra-op thread count to the node's CPUs (threads started later
+    inherit the affinity, so a larger pool would oversubscribe the node); ``log``: report the binding."""
     if len(glob.glob("/sys/devices/system/node/node[0-9]*")) < 2:
         return None
     node = gpu_numa_node(device)
@@ -61,4 +63,14 @@ def bind_to_gpu(device) -> Optional[int]:
         return None
     if cpus != allowed:
         os.sched_setaffinity(0, cpus)
+    if match_torch_threads:
+        import torch
+
+        if torch.get_num_threads() > len(cpus):
+            torch.set_num_threads(len(cpus))
+    if log:
+        import logging
+
+        logging.getLogger(__name__).info("bound the staging thread to NUMA node %d (%d CPUs) of %s", node,
+                                         len(cpus), device)
     return node

@@ -135,6 +135,10 @@ int64_t fa_qfed_launches(int64_t ld, int64_t P, int32_t chain);
  * window's per-workgroup partial norms: the gathers then run after every window).  fa_qfed_workspace_bytes(K, ld,
  * P) holds every window's partials of a call at (ld, P), chain or not: the gathers then run once per call
  * (ABI 3; the per-window form cost ~13 us a window).  Either way the norms are the same bits.
+ * Reproducibility: a call's results are the same bits run to run (fixed grid, fixed gather order, no atomics).
+ * delta and chain are per column, so calls with and without `chain` give the same delta bits; sqnorm is NOT
+ * bit-reproducible across that choice — chain launches sum each client's squares over 8-float4 tiles, plain ones
+ * over 16-float4 tiles (another fp64 order; ~1e-16 relative, the fp32 value hs consumes within one ulp).
  */
 int fa_qfed_max_chunk(void);
 int64_t fa_qfed_workspace_bytes(int32_t K, int64_t ld, int64_t P);

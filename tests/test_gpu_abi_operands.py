@@ -75,8 +75,8 @@ def _cases(dev, st):
                         p["sqnorm"], p["workspace"], ws_q, ACC, st)),
         Case("fa_qfed_hs", dict(sqnorm=f(K, 1.0, torch.float64), c1=f(K, 1.0), c2=f(K, 1.0), hs_out=f(2)), ["hs_out"],
              lambda p: (p["sqnorm"], p["c1"], p["c2"], K, p["hs_out"], st)),
-        Case("fa_qfed_finalize", dict(last=f(LD), delta=f(LD), hs=f(2, 2.0), out=f(LD)), ["out"],
-             lambda p: (p["last"], p["delta"], p["hs"], p["out"], P, st)),
+        Case("fa_qfed_finalize", dict(last=f(LD), delta=f(LD), hs_dev=f(2, 2.0), out=f(LD)), ["out"],
+             lambda p: (p["last"], p["delta"], p["hs_dev"], p["out"], P, st)),
         Case("fa_sum_rows_f64", dict(x=f(2 * K, 1.0, torch.float64), out=f(K, 0.0, torch.float64)), ["out"],
              lambda p: (p["x"], K, 2, K, p["out"], st)),
         Case("fa_side_accumulate", dict(xi=f(K * Q, 3, torch.int64), w=f(K, 1.0, torch.float64),
@@ -95,34 +95,35 @@ def _cases(dev, st):
              ["delta_s", "sqnorm"],
              lambda p: (p["xi"], Q, K, Q, p["last"], p["alpha"], ctypes.c_float(0.05), p["delta_s"], p["sqnorm"], 0,
                         st)),
-        Case("fa_side_qfed_finalize", dict(last=f(Q, 1, torch.int64), delta_s=f(Q), hs=f(2, 2.0),
+        Case("fa_side_qfed_finalize", dict(last=f(Q, 1, torch.int64), delta_s=f(Q), hs_dev=f(2, 2.0),
                                            model=f(Q, 5, torch.int64)), ["model"],
-             lambda p: (p["last"], p["delta_s"], p["hs"], p["model"], Q, st)),
+             lambda p: (p["last"], p["delta_s"], p["hs_dev"], p["model"], Q, st)),
         Case("fa_fill_synthetic", dict(x=f(K * LD)), ["x"],
              lambda p: (p["x"], LD, K, P, 1, 0, ctypes.c_float(0.05), ctypes.c_float(0.01), st)),
         Case("fa_prefix_box_combine",
              dict(xs=f(K * 16, 1.0), desc=box_desc + 0, tensors=torch.tensor([0, 1, 4, 1], dtype=torch.int64,
                                                                                device=dev),
                   chunk_tensor=torch.tensor([0, -1], dtype=torch.int32, device=dev),
-                  chunk_first=torch.tensor([0], dtype=torch.int64, device=dev), glob=f(4)), ["glob"],
-             lambda p: (p["xs"], p["desc"], K, p["tensors"], 1, p["chunk_tensor"], p["chunk_first"], 1, p["glob"], st)),
+                  chunk_first=torch.tensor([0], dtype=torch.int64, device=dev), **{"global": f(4)}), ["global"],
+             lambda p: (p["xs"], p["desc"], K, p["tensors"], 1, p["chunk_tensor"], p["chunk_first"], 1, p["global"],
+                        st)),
         Case("fa_dp_normals", dict(out=f(64)), ["out"], lambda p: (p["out"], 64, 5, 0, st)),
         # client-side pointer tables (include/fedclient.h)
-        Case("fa_prox_update", dict(param=tab(1.0), glob=tab(2.0)), ["param"],
-             lambda p: (t(p["param"]), t(p["glob"]), numel.ctypes.data, 2, ctypes.c_float(0.1), st)),
-        Case("fa_sgd_prox_step", dict(param=tab(1.0), grad=tab(0.5), buf=tab(0.0), glob=tab(2.0)), ["param", "buf"],
-             lambda p: (t(p["param"]), t(p["grad"]), t(p["buf"]), t(p["glob"]), numel.ctypes.data, 2,
+        Case("fa_prox_update", {"param": tab(1.0), "global": tab(2.0)}, ["param"],
+             lambda p: (t(p["param"]), t(p["global"]), numel.ctypes.data, 2, ctypes.c_float(0.1), st)),
+        Case("fa_sgd_prox_step", {"param": tab(1.0), "grad": tab(0.5), "momentum_buf": tab(0.0), "global": tab(2.0)}, ["param", "momentum_buf"],
+             lambda p: (t(p["param"]), t(p["grad"]), t(p["momentum_buf"]), t(p["global"]), numel.ctypes.data, 2,
                         ctypes.c_float(0.1), ctypes.c_float(0.9), ctypes.c_double(0.0), ctypes.c_float(5e-4), 0, 0,
                         ctypes.c_float(0.01), 1, st)),
-        Case("fa_sgd_prox_step_groups", dict(param=tab(1.0), grad=tab(0.5), buf=tab(0.0), glob=tab(2.0)),
-             ["param", "buf"],
-             lambda p: (t(p["param"]), t(p["grad"]), t(p["buf"]), t(p["glob"]), numel.ctypes.data, 2,
+        Case("fa_sgd_prox_step_groups", {"param": tab(1.0), "grad": tab(0.5), "momentum_buf": tab(0.0), "global": tab(2.0)},
+             ["param", "momentum_buf"],
+             lambda p: (t(p["param"]), t(p["grad"]), t(p["momentum_buf"]), t(p["global"]), numel.ctypes.data, 2,
                         host(np.float32, [0.1, 0.2]), host(np.float32, [0.9, 0.9]), host(np.float64, [0.0, 0.0]),
                         host(np.float32, [5e-4, 0.0]), host(np.int32, [0, 0]), ctypes.c_float(0.01), 1, st)),
         Case("fa_dp_clip_coef", dict(param=tab(1.0), last=tab(0.5), workspace=f(ws_dp // 8 + 1, 0.0, torch.float64),
-                                     coef=f(3)), ["coef"],
+                                     coef_out=f(3)), ["coef_out"],
              lambda p: (t(p["param"]), t(p["last"]), numel.ctypes.data, 2, ctypes.c_float(1.0), 0, p["workspace"],
-                        p["coef"], st)),
+                        p["coef_out"], st)),
         Case("fa_dp_apply", dict(param=tab(1.0), last=tab(0.5), upload=tab(0.0), coef=f(3, 0.5)), ["param", "upload"],
              lambda p: (t(p["param"]), t(p["last"]), t(p["upload"]), numel.ctypes.data, t([0, 40]), 2, p["coef"],
                         ctypes.c_float(0.1), 3, 1, st)),

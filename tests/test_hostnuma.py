@@ -47,3 +47,21 @@ def test_no_gpu_means_no_node():
     if torch.cuda.is_available():
         pytest.skip("a GPU is present")
     assert hostnuma.gpu_numa_node("cuda:0") is None
+
+
+def test_binding_lowers_torch_threads_to_the_node(two_nodes, monkeypatch):
+    """threads started after the binding inherit it, so torch's pool is cut to the node's CPUs."""
+    import torch
+
+    monkeypatch.setattr(hostnuma, "gpu_numa_node", lambda d: 1)
+    set_calls = []
+    monkeypatch.setattr(torch, "get_num_threads", lambda: 16)
+    monkeypatch.setattr(torch, "set_num_threads", lambda n: set_calls.append(n))
+    assert hostnuma.bind_to_gpu("cuda:0", match_torch_threads=True, log=True) == 1
+    assert two_nodes == [{4, 5}] and set_calls == [2]
+
+
+def test_mixin_numa_binding_is_opt_in():
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregatorMixin
+
+    assert DeviceAggregatorMixin.device_numa_bind is False

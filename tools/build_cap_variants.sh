@@ -8,7 +8,7 @@ cd /tmp
 for spec in "$@"; do
   IFS=, read S C <<< "$spec"
   C=${C:-75}
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -DFA_TUNING=1 \
     -DFA_CAP_SW_MAX=$S -DFA_GRID_CAP_PCT=$C \
     -o $ROOT/fedscale_amd/variants/libfedagg_cap_sw${S}_c${C}.so $ROOT/fedscale_amd/csrc/fedagg.hip &
 done

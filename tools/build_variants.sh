@@ -13,7 +13,7 @@ for spec in "$@"; do
   G=${G:-0}
   PP=${PP:-0}
   out=$ROOT/fedscale_amd/variants/libfedagg_v${V}_u${U}_nt${NT}_w${W}_g${G}_p${PP}.so
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -DFA_TUNING=1 \
     -DFA_RED_V=$V -DFA_RED_U=$U -DFA_RED_NT=$NT -DFA_RED_WAVES=$W -DFA_RED_GRID=$G -DFA_PIPE=$PP \
     -o $out $ROOT/fedscale_amd/csrc/fedagg.hip &
 done
