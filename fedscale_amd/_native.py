@@ -60,6 +60,9 @@ SIGNATURES = {
     "fa_side_qfed_finalize": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p]),
     "fa_fill_synthetic": (_i32, [_c_void_p, _i64, _i32, _i64, _u32, _i32, _f32, _f32, _c_void_p]),
     "fa_host_gather": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _i32]),
+    "fa_host_register": (_i32, [_c_void_p, _i64]),
+    "fa_host_unregister": (_i32, [_c_void_p]),
+    "fa_h2d_pieces": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _c_void_p, _i32]),
     "fa_pickle_strip": (_i64, [_c_void_p, _i64, _i64, _c_void_p, _i64, _c_void_p, _i32, _c_void_p]),
     "fa_prefix_box_combine": (_i32, [_c_void_p, _c_void_p, _i32, _c_void_p, _i32, _c_void_p, _c_void_p, _i32,
                                      _c_void_p, _c_void_p]),

@@ -13,6 +13,7 @@ HBM layout:
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence, Tuple
@@ -229,6 +230,67 @@ class HostRow:
         self.pending = []
 
 
+class RegisteredUpload:
+    """One arriving update whose LARGE fp32 entries the GPUs' copy engines read straight out of the host memory
+    that holds them — the executor's payload, registered in place (``fa_host_register``) — while the small
+    entries and the side table are gathered into a pinned ``row`` (round 4, N-GPU ingress: one host-DRAM pass per
+    large byte instead of three).  ``segs``: the whole-model segments (row offset, elements, large-entry index or
+    -1 for "from the row"), fixed per layout; ``src``: the address of every large entry's first element.  Each
+    part's ``ClientStaging.put`` copies the pieces of its slice and appends its event to ``events`` (and to the
+    row's ``pending``); the registration is released once they have all completed."""
+
+    __slots__ = ("row", "segs", "src", "events")
+
+    def __init__(self, row: "HostRow", segs, src: np.ndarray):
+        self.row, self.segs, self.src, self.events = row, segs, src, []
+
+
+class PieceSegments:
+    """Whole-model segments of a layout for ``RegisteredUpload``: fp32 entries of at least ``min_bytes`` are their
+    own segment (read from the registered upload), runs of smaller entries one segment each (read from the pinned
+    row).  ``large``: the fp32-entry positions (in ``layout.f_entries`` order) of the large entries."""
+
+    def __init__(self, layout: "BucketLayout", min_bytes: int):
+        if layout.world != 1:
+            raise ValueError("PieceSegments: a whole-model layout (the coordinator's)")
+        self.large = [j for j, e in enumerate(layout.f_entries) if e.numel and 4 * e.numel >= min_bytes]
+        li = {j: n for n, j in enumerate(self.large)}
+        segs = []
+        for j, e in enumerate(layout.f_entries):
+            if e.numel == 0:
+                continue
+            if j in li:
+                segs.append((e.offset, e.numel, li[j]))
+            elif segs and segs[-1][2] < 0 and segs[-1][0] + segs[-1][1] == e.offset:
+                segs[-1] = (segs[-1][0], segs[-1][1] + e.numel, -1)
+            else:
+                segs.append((e.offset, e.numel, -1))
+        self.segs = segs
+        # positions in host_gather_plan's piece lists (one piece per NON-EMPTY fp32 entry of a whole-model layout)
+        piece, k = {}, 0
+        for j, e in enumerate(layout.f_entries):
+            if e.numel:
+                piece[j] = k
+                k += 1
+        self.large_pieces = [piece[j] for j in self.large]
+        self.small_pieces = np.asarray([piece[j] for j in piece if j not in li], dtype=np.int64)
+
+    def part_plan(self, p0: int, p1: int):
+        """(dst byte offsets in the part's row, byte counts, large index or -1, source byte offsets) of the pieces
+        of slice [p0, p1): relative to the large entry's first byte, or to the start of the pinned row."""
+        dst, nb, kind, soff = [], [], [], []
+        for off, n, k in self.segs:
+            lo, hi = max(off, p0), min(off + n, p1)
+            if lo >= hi:
+                continue
+            dst.append(4 * (lo - p0))
+            nb.append(4 * (hi - lo))
+            kind.append(k)
+            soff.append(4 * (lo - off) if k >= 0 else 4 * lo)
+        return (np.asarray(dst, dtype=np.uint64), np.asarray(nb, dtype=np.int64), np.asarray(kind, dtype=np.int64),
+                np.asarray(soff, dtype=np.uint64))
+
+
 class ClientStaging:
     """Device staging area for up to ``capacity`` client updates of one round (chunk).
 
@@ -325,6 +387,8 @@ class ClientStaging:
     def put(self, slot: int, update):
         if type(update) is HostRow:
             return self._put_row(slot, update)
+        if type(update) is RegisteredUpload:
+            return self._put_registered(slot, update)
         lay = self.layout
         values = lay.values_of(update)
         if self.bulk and self._views is not None and self._put_bulk_views(slot, values):
@@ -385,6 +449,43 @@ class ClientStaging:
                 ev = self._row_evs[id(row)] = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self._dev_index))
         row.pending.append(ev)
+
+    def _put_registered(self, slot: int, up: "RegisteredUpload"):
+        """This part's slice of an upload read partly from its registered host memory (``RegisteredUpload``):
+        one native call enqueues every piece's H2D on this device's stream (``fa_h2d_pieces``)."""
+        from . import _native
+
+        lay = self.layout
+        plan = getattr(self, "_reg_plan", None)
+        if plan is None or plan[0] is not up.segs:
+            plan = self._reg_plan = (up.segs, up.segs.part_plan(lay.p0, lay.p1))
+        dst, nb, kind, soff = plan[1]
+        rowbase = np.uint64(up.row.f.data_ptr())
+        src = np.where(kind >= 0, up.src[np.maximum(kind, 0)] + soff, rowbase + soff).astype(np.uint64)
+        if self.bulk:  # a small staging area keeps its pinned mirror: the pieces are host copies into it
+            self._claim_bulk(slot)
+            mirror = self._hx_np[slot]
+            for d, n, s_ in zip(dst.tolist(), nb.tolist(), src.tolist()):
+                ctypes_src = np.ctypeslib.as_array((ctypes.c_float * (n // 4)).from_address(s_))
+                mirror[d // 4:(d + n) // 4] = ctypes_src
+            if lay.Q:
+                self._hxi_np[slot, :lay.Q] = up.row.i_np[:lay.Q]
+            self._bulk_hi = slot + 1
+            return
+        with self._on():
+            st = torch.cuda.current_stream(self._dev_index)
+            if len(nb):
+                dsts = (np.uint64(self.x[slot].data_ptr()) + dst).astype(np.uint64)
+                sidx = np.zeros(len(nb), dtype=np.int32)
+                streams = np.asarray([st.cuda_stream], dtype=np.uint64)
+                _native.call("fa_h2d_pieces", dsts.ctypes.data, src.ctypes.data, nb.ctypes.data, sidx.ctypes.data,
+                             len(nb), streams.ctypes.data, 1)
+            if lay.Q:
+                self.xi[slot, :lay.Q].copy_(up.row.i[:lay.Q], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        up.row.pending.append(ev)
+        up.events.append(ev)
 
     def _put_bulk_views(self, slot: int, values) -> bool:
         """Small whole-model update of plain numpy arrays: validate (shape, dtype) and copy each entry into

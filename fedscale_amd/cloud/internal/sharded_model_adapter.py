@@ -33,7 +33,7 @@ from typing import Optional
 import numpy as np
 import torch
 
-from ...bucket import BucketLayout, HostRow, default_pack_workers
+from ...bucket import BucketLayout, HostRow, PieceSegments, RegisteredUpload, default_pack_workers
 from ...round import default_capacity
 from ...state import DeviceGroup, PartOf, ShardGroup
 from .torch_model_adapter import TorchModelAdapter
@@ -71,6 +71,14 @@ class ShardedModelAdapter(TorchModelAdapter):
     #: pinned full-model rows an upload is gathered into before the per-device copies (the host packs
     #: update k+1 while update k is still crossing PCIe)
     INGRESS_ROWS = 2
+    #: round 4: an upload whose large arrays all view ONE host buffer (the executor's payload decoded zero-copy by
+    #: the mixin's deserialize_response, fedscale_amd/ingress.py) has that buffer registered in place, and every
+    #: GPU's copy engine reads its slice of the large arrays straight out of it (``RegisteredUpload``): one
+    #: host-DRAM pass per byte instead of three (profiles/r04_register_probe.log).  Entries below this size, and
+    #: uploads that do not qualify, take the pinned-row gather.  -1 turns it off.
+    REGISTER_MIN_ENTRY_BYTES = 1 << 20
+    #: registrations kept while their copies may still run (older ones are waited for and released first)
+    REGISTER_MAX_PENDING = 4
 
     def __init__(self, model: torch.nn.Module, optimizer=None, devices=None, staging_capacity: Optional[int] = None,
                  transport: Optional[str] = None):
@@ -92,6 +100,10 @@ class ShardedModelAdapter(TorchModelAdapter):
                                                 staging_capacity=staging_capacity, dstream=self.group.streams[r]))
         self._rows = []
         self._next_row = 0
+        self._regs = {}  # registered address -> [payload object, events of the copies out of it]
+        self._reg_segs = None
+        self._reg_failed = False
+        self.registered_uploads = 0  # uploads staged out of their registered payload (the rest: pinned-row gather)
         self.pack_workers = default_pack_workers()
         self._init_egress(True)
         self._egress_src = self._part_buffers()
@@ -102,8 +114,10 @@ class ShardedModelAdapter(TorchModelAdapter):
 
     def close(self):
         """Destroy the device group's RCCL communicator now (its HBM and proxy threads) rather than at interpreter
-        exit, where ``state._LIVE_GROUPS`` would otherwise hold it.  Idempotent; the adapter stays usable (the next
-        collective re-creates the communicator).  Call it from the thread that drives the rounds."""
+        exit, where ``state._LIVE_GROUPS`` would otherwise hold it, and release every registered upload (after its
+        copies).  Idempotent; the adapter stays usable (the next collective re-creates the communicator).  Call it
+        from the thread that drives the rounds."""
+        self._release_registrations(block=True)
         self.group.close()
 
     def __enter__(self):
@@ -113,18 +127,89 @@ class ShardedModelAdapter(TorchModelAdapter):
         self.close()
 
     # ---- ingress ----------------------------------------------------------------------------------
-    def _stage_row(self, update) -> HostRow:
+    def _stage_row(self, update):
         """Gather one upload into the next pinned full-model row (validated like the reference's list
-        handling, aggregator.py:494-496; multi-threaded native gather)."""
+        handling, aggregator.py:494-496; multi-threaded native gather) — or, when its large arrays view one
+        registrable host buffer, only its small entries (``RegisteredUpload``)."""
         L = self.layout
         if not self._rows:
             self._rows = [HostRow(L.ld, L.ldq) for _ in range(self.INGRESS_ROWS)]
         row = self._rows[self._next_row]
         plan = L.host_gather_plan(L.values_of(update))
+        reg = self._register(plan)
         row.wait()  # every part's H2D out of this row has completed
-        L.run_host_gather(plan, row.f_np, row.i_np, workers=self.pack_workers)
+        if reg is not None:
+            segs, src, addr = reg
+            ps, po, pn, keep, side = plan
+            small = segs.small_pieces
+            L.run_host_gather((ps[small], po[small], pn[small], keep, side), row.f_np, row.i_np,
+                              workers=self.pack_workers)
+            out = RegisteredUpload(row, segs, src)
+            self._regs[addr][1].append(out)
+            self.registered_uploads += 1
+        else:
+            L.run_host_gather(plan, row.f_np, row.i_np, workers=self.pack_workers)
+            out = row
         self._next_row = (self._next_row + 1) % len(self._rows)
-        return row
+        return out
+
+    def _register(self, plan):
+        """(segments, large-entry addresses, registered address) when the upload's large fp32 arrays all view one
+        host buffer that is (or now gets) registered; None: take the pinned-row gather."""
+        from ... import _native
+
+        if self.REGISTER_MIN_ENTRY_BYTES < 0 or self._reg_failed:
+            return None
+        if self._reg_segs is None:
+            self._reg_segs = PieceSegments(self.layout, self.REGISTER_MIN_ENTRY_BYTES)
+        segs = self._reg_segs
+        if not segs.large:
+            return None
+        ps, po, pn, keep, side = plan
+        root = None
+        for j in segs.large_pieces:  # the arrays as handed in (host_gather_plan keeps them, contiguous)
+            r = keep[j]
+            while isinstance(r.base, np.ndarray):
+                r = r.base
+            r = r.base
+            if r is None or (root is not None and r is not root):
+                return None
+            root = r
+        try:
+            buf = np.frombuffer(root, dtype=np.uint8)
+        except (TypeError, ValueError):
+            return None
+        lo, n = buf.ctypes.data, buf.nbytes
+        page = 4096
+        a0, a1 = lo // page * page, -(-(lo + n) // page) * page  # whole pages of the payload's own mapping
+        self._release_registrations(block=False)
+        if a0 not in self._regs:
+            if len(self._regs) >= self.REGISTER_MAX_PENDING:
+                self._release_registrations(block=True, keep=self.REGISTER_MAX_PENDING - 1)
+            try:
+                _native.call("fa_host_register", a0, a1 - a0)
+            except _native.FedAggError:
+                self._reg_failed = True  # e.g. memory the runtime will not pin: the gather from now on
+                return None
+            self._regs[a0] = [root, []]
+        return segs, np.asarray([ps[j] for j in segs.large_pieces], dtype=np.uint64), a0
+
+    def _release_registrations(self, block: bool, keep: int = 0):
+        """Unregister uploads whose copies have all completed (``block``: wait for the oldest ones, until at most
+        ``keep`` remain)."""
+        from ... import _native
+
+        for addr in list(self._regs):
+            ups = self._regs[addr][1]
+            done = all(ev.query() for up in ups for ev in up.events)
+            if not done and block and len(self._regs) > keep:
+                for up in ups:
+                    for ev in up.events:
+                        ev.synchronize()
+                done = True
+            if done:
+                del self._regs[addr]
+                _native.call("fa_host_unregister", addr)
 
     # ---- rounds -----------------------------------------------------------------------------------
     def begin_round(self, K: int, policy: str, capacity: Optional[int] = None, keep_mean=True) -> ShardedRound:
@@ -148,6 +233,7 @@ class ShardedModelAdapter(TorchModelAdapter):
             for p, r in zip(self.parts, rnd.rounds):
                 p.apply_round(r, denom32, denom64, None, keep_mean)
         self._commit()
+        self._release_registrations(block=False)
 
     def _apply_qfed(self, rnd: ShardedRound):
         mode = getattr(self.optimizer, "mode", None)

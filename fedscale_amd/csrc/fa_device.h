@@ -120,7 +120,7 @@ class DevScope {
     const uintptr_t a = (uintptr_t)p;
     for (int i = 0; i < nr_; ++i) {  // most recent first: a table's consecutive tensors share a segment
       const Range& r = rng_[(last_ + nr_ - i) % kRanges];
-      if (a >= r.lo && a < r.hi && (r.host == 0 || host_ok)) {
+      if (a >= r.lo && a < r.hi && (r.host == 0 || (host_ok && r.host == 1))) {
         if (bytes > r.hi - a) return operr(name, "%s extends %llu bytes past the end of its allocation", bytes - (r.hi - a));
         return FA_OK;
       }
@@ -159,6 +159,37 @@ class DevScope {
     if (bytes > r.hi - a) return operr(name, "%s extends %llu bytes past the end of its allocation", bytes - (r.hi - a));
     return FA_OK;
   }
+  // the SOURCE of an H2D copy-engine transfer (fa_h2d_pieces): registered or pinned host memory — pageable memory
+  // would turn the async copy into a synchronous staged one — and inside its registration
+  int host_source(const char* name, const void* p, uint64_t bytes) {
+    if (!p || bytes == 0) return FA_OK;
+    const uintptr_t a = (uintptr_t)p;
+    for (int i = 0; i < nr_; ++i) {
+      const Range& r = rng_[(last_ + nr_ - i) % kRanges];
+      if (a >= r.lo && a < r.hi && r.host >= 1) {
+        if (bytes > r.hi - a) return operr(name, "%s extends %llu bytes past the end of its registration", bytes - (r.hi - a));
+        return FA_OK;
+      }
+    }
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess || at.type != hipMemoryTypeHost) {
+      (void)hipGetLastError();
+      return operr(name, "%s is not registered (fa_host_register) or pinned host memory", 0);
+    }
+    void* base = nullptr;
+    size_t size = 0;
+    if (hipMemGetAddressRange((hipDeviceptr_t*)&base, &size, (hipDeviceptr_t)p) != hipSuccess || !base) {
+      (void)hipGetLastError();
+      return operr(name, "%s: no registration range for the pointer", 0);
+    }
+    const Range r{(uintptr_t)base, (uintptr_t)base + size, 2};
+    if (a < r.lo || a >= r.hi) return operr(name, "%s lies outside the registration HIP reports for it", 0);
+    last_ = (last_ + 1) % kRanges;
+    rng_[last_] = r;
+    if (nr_ < kRanges) ++nr_;
+    if (bytes > r.hi - a) return operr(name, "%s extends %llu bytes past the end of its registration", bytes - (r.hi - a));
+    return FA_OK;
+  }
   // a HOST table of n device pointers, tensor i holding numel[i] elements of elem_bytes (numel[i] == 0: skipped)
   int table(const char* name, const void* const* ptrs, const int64_t* numel, int n, int elem_bytes,
             bool host_ok = false) {
@@ -168,7 +199,7 @@ class DevScope {
       if (numel[i] <= 0 || !ptrs[i]) continue;
       const uintptr_t a = (uintptr_t)ptrs[i];
       const Range& r = rng_[last_];  // fast path: the same segment as the previous tensor
-      if (nr_ > 0 && a >= r.lo && a < r.hi && (r.host == 0 || host_ok) &&
+      if (nr_ > 0 && a >= r.lo && a < r.hi && (r.host == 0 || (host_ok && r.host == 1)) &&
           (uint64_t)numel[i] * elem_bytes <= r.hi - a)
         continue;
       snprintf(nm, sizeof(nm), "%s[%d]", name, i);
@@ -193,7 +224,7 @@ class DevScope {
   }
   struct Range {
     uintptr_t lo, hi;
-    int host;  // 1: pinned host memory
+    int host;  // 1: pinned host memory mapped at the same address; 2: host memory only known to be registered
   };
   static constexpr int kRanges = 16;
   Range rng_[kRanges] = {};

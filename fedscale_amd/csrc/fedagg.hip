@@ -840,9 +840,20 @@ __device__ __forceinline__ float fast_div(float a, float b, float r) {
 #ifndef QF_PART
 #define QF_PART 4
 #endif
+// The chain launches' own knobs (round 4).  Round 2 kept them equal to the plain launches' so that both summed
+// the norms identically; since round 3's 8-float4 chain tiles sum them in another fp64 order anyway, the chain
+// launches take the cheaper forms: the range test on max |a| alone and fp32 partials of 8 squares — one v_max3
+// per two elements and one cvt + fp64 add per 8 squares fewer.  Measured interleaved on one box
+// (tools/tune_qfed2.py, profiles/r04_tune_qfed_chain_knobs.log): 1024 x 12.5 M 7.354 -> 7.185 ms (first pass) and
+// 7.361 -> 7.185 ms (later passes), 1000 x 25 M 14.47 -> 14.06 ms; the chain launches now read faster than the
+// plain ones.  The norms move by <= 1e-10 relative (the fp32 value hs consumes: at most one ulp).
 #ifndef QF_CHAIN_EMAX
-#define QF_CHAIN_EMAX QF_EMAX  // the bound test of the chain launches (round 3: their own knob)
+#define QF_CHAIN_EMAX 0
 #endif
+#ifndef QF_CHAIN_PART
+#define QF_CHAIN_PART 8
+#endif
+static_assert(QF_CHAIN_PART == 4 || QF_CHAIN_PART == 8 || QF_CHAIN_PART == 16, "QF_CHAIN_PART: 4, 8 or 16");
 static_assert(QF_PART == 4 || QF_PART == 8 || QF_PART == 16, "QF_PART: 4, 8 or 16");
 // EMAX picks which bound test admits an element to the fast division; both tests admit only elements the
 // fast division gets correctly rounded, so the choice never changes a bit, only the VALU count.
@@ -959,17 +970,19 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
         rng.add(t[j].z);
         rng.add(t[j].w);
       }
+      constexpr int PART = CHAIN ? QF_CHAIN_PART : QF_PART;
+      static_assert(QV % (PART / 4) == 0, "a tile's float4 columns split into whole partials");
       double acc = 0.0;
 #pragma unroll
-      for (int j = 0; j < QV; j += QF_PART / 4) {
+      for (int j = 0; j < QV; j += PART / 4) {
         float s = 0.f;
 #pragma unroll
-        for (int i = 0; i < QF_PART / 4; ++i) {
+        for (int i = 0; i < PART / 4; ++i) {
           const f4 g2 = g[j + i] * g[j + i];  // torch.square(grad), fp32
           const float s4 = (g2.x + g2.y) + (g2.z + g2.w);
           s = i == 0 ? s4 : s + s4;
         }
-        acc += (double)s;  // QF_PART-term fp32 partial, then fp64
+        acc += (double)s;  // PART-term fp32 partial, then fp64
       }
 #if QF_INFCHK == 1
       const bool fast_ok = rng.ok();
@@ -986,10 +999,10 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
           g[j].w = __fdiv_rn(t[j].w, q.lr);
         }
 #pragma unroll
-        for (int j = 0; j < QV; j += QF_PART / 4) {  // the same partials as the fast path
+        for (int j = 0; j < QV; j += PART / 4) {  // the same partials as the fast path
           float s = 0.f;
 #pragma unroll
-          for (int i = 0; i < QF_PART / 4; ++i) {
+          for (int i = 0; i < PART / 4; ++i) {
             const f4 g2 = g[j + i] * g[j + i];
             const float s4 = (g2.x + g2.y) + (g2.z + g2.w);
             s = i == 0 ? s4 : s + s4;

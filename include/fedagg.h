@@ -18,6 +18,10 @@
  *     GPU — the library makes it current for the call and restores the caller's current device after, so
  *     one host thread can drive several GPUs (fedscale_amd/csrc/fa_device.h).  Launch plans size their
  *     grids by that GPU's CU count.
+ *   - operands (ABI 3, round 4): before anything is queued, EVERY buffer a call's kernels read or write is
+ *     checked to be device memory of the call's GPU — or pinned host memory where an entry point says so —
+ *     and to hold the call's extent inside its allocation; otherwise FA_E_ARG names the operand and nothing
+ *     is launched (pageable memory would fault the GPU; another GPU's memory would be read over xGMI).
  *   - a "bucket" is the fp32 tensors of a state_dict concatenated in state_dict order: P elements,
  *     padded with zeros to a row stride `ld` (multiple of 64).  Client updates live client-major,
  *     x[k*ld + p].  Every per-column buffer (acc, out, last, m, v, delta) holds >= round_up(P, 4)
@@ -225,6 +229,22 @@ int fa_prefix_box_combine(const float* xs, const int64_t* desc, int32_t K, const
  */
 int fa_host_gather(void* dst, const void* const* srcs, const int64_t* dst_off, const int64_t* nbytes, int32_t n,
                    int32_t threads);
+
+/*
+ * N-GPU ingress straight out of the upload's own bytes (round 4; replaces, for a model sharded over several
+ * GPUs of the one aggregator process, the pinned full-model row that fa_host_gather fills: one host-DRAM pass per
+ * byte instead of three).  fa_host_register pins and registers the pages of host memory the caller owns — the
+ * executor's pickled payload whose arrays fedscale_amd/ingress.py decoded as views (aggregator.py:704) — and
+ * fa_host_unregister releases them once every copy out of them has completed.  fa_h2d_pieces enqueues, for each
+ * piece i, an asynchronous H2D copy of nbytes[i] from src[i] to dst[i] on streams[sidx[i]] (a HOST table of
+ * nstreams hipStream_t): dst[i] must be device memory of that stream's device, src[i] registered or pinned host
+ * memory, both holding nbytes[i] — checked for every piece before any copy is enqueued (FA_E_ARG otherwise).
+ * Copies run in piece order per stream.  No reference counterpart (the reference has no device, aggregator.py).
+ */
+int fa_host_register(void* p, int64_t nbytes);
+int fa_host_unregister(void* p);
+int fa_h2d_pieces(void* const* dst, const void* const* src, const int64_t* nbytes, const int32_t* sidx, int32_t n,
+                  void* const* streams, int32_t nstreams);
 
 /*
  * Host ingress (no GPU work): strip the large byte strings out of a pickled executor result so it can be

@@ -224,21 +224,35 @@ def test_pinned_host_operand_only_where_the_header_allows_it(gpu_device):
 
 
 def test_operand_extent_beyond_its_allocation_is_rejected(gpu_device):
-    """A buffer too short for the call (here: P columns over a tensor of P/2) is refused, not overrun."""
+    """A buffer too short for the call (here: P columns over an allocation of P/2) is refused, not overrun.  The
+    short operand is its own hipMalloc (torch's caching allocator would hand out a slice of a larger segment)."""
     from fedscale_amd import _native as N
 
     lib = N.load()
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
+    hip.hipFree.argtypes = [ctypes.c_void_p]
     st = torch.cuda.current_stream().cuda_stream
-    big = 1 << 22  # its own caching-allocator segment, so the allocation ends where the tensor does
+    big = 1 << 22
     cur = torch.ones(big, device=gpu_device)
-    short = torch.ones(big // 2, device=gpu_device)
     m, v, out = (torch.zeros(big, device=gpu_device) for _ in range(3))
-    rc = lib.fa_yogi_step(cur.data_ptr(), short.data_ptr(), m.data_ptr(), v.data_ptr(), out.data_ptr(), big,
-                          3e-3, 1e-8, 0.9, 0.1, 0.01, 0, st)
-    msg = lib.fa_last_error_string().decode()
-    assert rc == -1 and "last" in msg and "past the end of its allocation" in msg, msg
-    torch.cuda.synchronize()
-    assert int(torch.count_nonzero(out)) == 0
+    short = ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(short), big // 2 * 4) == 0
+    hip.hipMemset.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t]
+    assert hip.hipMemset(short, 0, big // 2 * 4) == 0
+    try:
+        rc = lib.fa_yogi_step(cur.data_ptr(), short.value, m.data_ptr(), v.data_ptr(), out.data_ptr(), big,
+                              3e-3, 1e-8, 0.9, 0.1, 0.01, 0, st)
+        msg = lib.fa_last_error_string().decode()
+        assert rc == -1 and "last" in msg and "past the end of its allocation" in msg, msg
+        rc = lib.fa_yogi_step(cur.data_ptr(), short.value, m.data_ptr(), v.data_ptr(), out.data_ptr(), big // 2,
+                              3e-3, 1e-8, 0.9, 0.1, 0.01, 0, st)  # the same operand, within its allocation
+        assert rc == 0, lib.fa_last_error_string().decode()
+        torch.cuda.synchronize()
+        assert int(torch.count_nonzero(out[big // 2:])) == 0 and int(torch.count_nonzero(out[:big // 2])) > 0
+    finally:
+        torch.cuda.synchronize()
+        hip.hipFree(short)
 
 
 def test_rccl_buffers_are_checked(gpu_device):
@@ -248,7 +262,8 @@ def test_rccl_buffers_are_checked(gpu_device):
     if not lib.fa_rccl_available():
         pytest.skip("RCCL not loadable")
     comm = ctypes.c_void_p()
-    N.call("fa_rccl_init", 1, _u64([0]).astype(np.int32).ctypes.data, ctypes.byref(comm))
+    devs = np.zeros(1, dtype=np.int32)
+    N.call("fa_rccl_init", 1, devs.ctypes.data, ctypes.byref(comm))
     try:
         st = torch.cuda.current_stream().cuda_stream
         send = torch.ones(64, device=gpu_device)
@@ -257,16 +272,15 @@ def test_rccl_buffers_are_checked(gpu_device):
         sts = _u64([st])
         for s_ptr, r_ptr, name in ((pageable.ctypes.data, recv.data_ptr(), "send[0]"),
                                    (send.data_ptr(), pageable.ctypes.data, "recv[0]")):
-            rc = lib.fa_rccl_all_reduce(comm, _u64([s_ptr]).ctypes.data, _u64([r_ptr]).ctypes.data, 64, N.FA_DT_F32,
+            st_tab, rt_tab = _u64([s_ptr]), _u64([r_ptr])  # held: the library reads the tables during the call
+            rc = lib.fa_rccl_all_reduce(comm, st_tab.ctypes.data, rt_tab.ctypes.data, 64, N.FA_DT_F32,
                                         sts.ctypes.data)
             msg = lib.fa_last_error_string().decode()
             assert rc == -1 and name in msg and "pageable" in msg, msg
-        short = torch.zeros(16, device=gpu_device)
-        del short  # (a recv buffer shorter than the gather is refused by its extent, covered on the CPU)
         torch.cuda.synchronize()
         assert int(torch.count_nonzero(recv)) == 0
-        N.call("fa_rccl_all_reduce", comm, _u64([send.data_ptr()]).ctypes.data, _u64([recv.data_ptr()]).ctypes.data,
-               64, N.FA_DT_F32, sts.ctypes.data)
+        st_tab, rt_tab = _u64([send.data_ptr()]), _u64([recv.data_ptr()])
+        N.call("fa_rccl_all_reduce", comm, st_tab.ctypes.data, rt_tab.ctypes.data, 64, N.FA_DT_F32, sts.ctypes.data)
         torch.cuda.synchronize()
         assert torch.equal(recv, send)
     finally:

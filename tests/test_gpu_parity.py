@@ -637,10 +637,10 @@ def test_qfed_fused_chain_kernel(gpu_device, K, P):
     """fa_qfed_accumulate with the fused FedAvg chain (LDS-DMA prefetch kernel on QF_CHAIN_V = 8-float4 tiles):
     delta equals the plain launch's bit for bit, the chain equals fa_reduce's FedAvg sum of the same rows bit for
     bit, and a chunked launch pair continues both chains exactly (FA_ACCUMULATE).  The per-client squared norms
-    are summed over tiles of another width (the plain kernel's are 16 float4 wide), i.e. in another fp64 order:
-    chain and plain launches are NOT bit-reproducible against each other on the norms (include/fedagg.h).  Their
-    fp64 sums agree to ~1e-16 relative, so their fp32 roundings (what hs consumes, optimizers.py:97's torch.sum of
-    fp32) agree to 1 ulp — equal unless a sum falls next to an fp32 rounding tie."""
+    are summed over tiles of another width (the plain kernel's are 16 float4 wide) from fp32 partials of 8 squares
+    instead of 4 (QF_CHAIN_PART, round 4), i.e. in another order: chain and plain launches are NOT bit-reproducible
+    against each other on the norms (include/fedagg.h).  Their sums agree to ~1e-10 relative, so their fp32
+    roundings (what hs consumes, optimizers.py:97's torch.sum of fp32) agree to within one ulp."""
     from fedscale_amd import kernels as kx
     from fedscale_amd import synth
     from fedscale_amd.bucket import round_up
@@ -669,7 +669,7 @@ def test_qfed_fused_chain_kernel(gpu_device, K, P):
     n1, n0 = outs[True][1], outs[False][1]
     f1, f0 = n1.float(), n0.float()
     assert bool((f1 == f0).logical_or(torch.nextafter(f0, f1) == f1).all())  # within one fp32 ulp
-    assert float(((n1 - n0).abs() / n0.abs().clamp_min(1e-300)).max()) < 1e-14
+    assert float(((n1 - n0).abs() / n0.abs().clamp_min(1e-300)).max()) < 1e-9
     want = torch.empty(ld, device="cuda")
     kx.reduce(x, K, P, want)
     assert torch.equal(outs[True][2], want[:P])

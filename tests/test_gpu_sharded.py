@@ -567,3 +567,102 @@ def test_selfcheck_module(gpu_device, devices):
     assert r.returncode == 0 and rep["ok"], rep
     assert set(rep["policies"]) == {"fedavg", "fedbuff", "fed-yogi", "q-fedavg"}
     assert all(v["calls_off_their_stream"] == 0 and v["native_calls"] > 0 for v in rep["policies"].values())
+
+
+@pytest.mark.parametrize("parts", [1, 2, 3])
+def test_adopt_resident_round_is_the_reference_mean(gpu_device, parts):
+    """The bench hook of the in-process N-GPU round (DeviceRound.adopt_resident, fedscale_amd/inproc_bench.py):
+    uploads written into every part's staging on its device, taken as the round's K arrivals, give the same
+    model as the sequential fp32 mean (aggregator.py:497-507) of the same synthetic rows, bit for bit; and
+    ShardedModelAdapter.close() releases the group and leaves the adapter usable."""
+    from fedscale_amd import synth
+    from fedscale_amd.cloud.internal.sharded_model_adapter import ShardedModelAdapter
+
+    K, P, seed = 9, 70_001, 31
+    model = synth.LayoutModule(["a", "b"], [(50_000,), (20_001,)], [torch.float32] * 2)
+    ad = ShardedModelAdapter(model, devices=[0] * parts, transport="copy", staging_capacity=K)
+    with ad:
+        for rep in range(2):
+            rnd = ad.begin_round(K, "fedavg", capacity=K)
+            for i, (p, r) in enumerate(zip(ad.parts, rnd.rounds)):
+                with p.dstream:
+                    x = r.staging.x
+                    # part i's slice of client k = columns [p0, p1) of the whole-model row
+                    full = torch.empty(K, -(-P // 64) * 64, device="cuda")
+                    synth.fill(full, K, P, seed=seed + rep)
+                    x[:, :p.layout.P].copy_(full[:, p.layout.p0:p.layout.p1])
+            rnd.adopt_resident(K)
+            with pytest.raises(ValueError):
+                rnd.adopt_resident(1)  # the round already has its K arrivals
+            ad.apply_round(rnd, float(np.float32(K)), float(K))
+            got = np.concatenate([w.numpy().reshape(-1) for w in ad.get_weights()])
+            acc = None
+            for row in synth.host_columns(seed + rep, range(K), np.arange(P)):
+                acc = row.copy() if acc is None else acc + row
+            np.testing.assert_array_equal(got, np.divide(acc, np.float32(K)))
+    ad.close()  # idempotent
+
+
+def test_inproc_bench_module_rehearsal(gpu_device):
+    """fedscale_amd.inproc_bench (what bench.py --gpus N runs on rank 0) on the one-GPU box: two parts on one card
+    and the one-GPU adapter beside them, small sizes; the report carries the fields bench.py records."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "fedscale_amd.inproc_bench", "--devices", "0,0", "--clients", "16",
+                        "--params", "1000000", "--rounds", "3"], cwd=root, capture_output=True, text=True,
+                       timeout=300)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines, (r.returncode, r.stderr[-2000:])
+    rep = json.loads(lines[-1])
+    assert r.returncode == 0 and rep["ok"], rep
+    assert rep["transport"] == "copy" and rep["distinct_gpus"] is False
+    assert len(rep["part_kernel_ms"]) == 2 and all(t > 0 for t in rep["part_kernel_ms"])
+    for k in ("inproc_round_ms", "egress_ms", "inproc_round_ms_incl_egress", "speedup_vs_one_gpu"):
+        assert rep[k] > 0, k
+    assert rep["one_gpu"]["round_ms"] > 0
+
+
+@pytest.mark.parametrize("parts", [2, 3])
+def test_registered_payload_ingress_is_bit_exact(gpu_device, parts):
+    """Round-4 N-GPU ingress: uploads decoded zero-copy from the executor's pickled payload (the mixin's
+    deserialize_response, aggregator.py:704) are registered in place and every part's copy engine reads its slice
+    of the large arrays straight out of the payload (RegisteredUpload, fa_h2d_pieces); small entries and int64
+    entries come from the pinned row.  Mixed with plain dict uploads (the gather path) in the same round, over
+    chunk folds: the model is the oracle's FedAvg mean bit for bit, and every registration is released."""
+    from fedscale_amd import ingress
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.sharded_model_adapter import ShardedModelAdapter
+    from oracle.cpu_reference import fedavg_close, fedavg_step
+
+    names = ["big0", "bn.running_mean", "bn.num_batches_tracked", "big1", "small", "big2"]
+    shapes = [(700, 1000), (64,), (), (300_001,), (5,), (1, 1_200_000)]
+    dtypes = [torch.float32, torch.float32, torch.int64, torch.float32, torch.float32, torch.float32]
+    init = [torch.zeros(s, dtype=d) for s, d in zip(shapes, dtypes)]
+    sharded = ShardedModelAdapter(StateDictModule(names, init), devices=[0] * parts, transport="copy",
+                                  staging_capacity=4)
+    agg = DeviceAggregator(sharded)
+    rng = np.random.default_rng(parts)
+    K = 11
+    for r in range(2):
+        agg.start_round(K)
+        acc = None
+        for k in range(K):
+            up = {}
+            for n, s, d in zip(names, shapes, dtypes):
+                up[n] = (np.array(int(rng.integers(0, 50)), dtype=np.int64).reshape(s) if d == torch.int64 else
+                         rng.standard_normal(s, dtype=np.float32))
+            acc = fedavg_step(acc, up, k == 0)
+            if k % 3 != 2:  # the deployed path: a pickled payload, decoded as views of its bytes
+                res = ingress.loads(pickle.dumps({"client_id": k, "update_weight": up, "moving_loss": 1.0}))
+                assert not res["update_weight"]["big0"].flags.owndata
+            else:
+                res = {"client_id": k, "update_weight": up, "moving_loss": 1.0}
+            agg.on_result(res)
+        assert_state_equal(sharded.get_weights(), fedavg_close(acc, K), f"round {r}")
+    assert sharded.registered_uploads == 2 * sum(1 for k in range(K) if k % 3 != 2)
+    sharded.close()
+    assert not sharded._regs

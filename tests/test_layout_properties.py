@@ -58,3 +58,40 @@ def test_client_blocks_partition_arrivals(K, world):
     for k in ks:
         a, b = blocks[g.owner(int(k), K)]
         assert a <= k < b
+
+
+def test_piece_segments_cover_every_slice_exactly():
+    """RegisteredUpload's segments (fedscale_amd/bucket.py PieceSegments, round-4 N-GPU ingress): the whole-model
+    segments tile [0, P) in order; each large entry is one segment; every part's pieces tile its slice [p0, p1)
+    exactly, each piece inside one segment; empty entries take no piece."""
+    import numpy as np
+    import torch
+
+    from fedscale_amd.bucket import BucketLayout, PieceSegments
+
+    rng = np.random.default_rng(3)
+    for trial in range(20):
+        T = int(rng.integers(1, 30))
+        shapes = [(int(rng.choice([0, 1, 7, 300, 70_000, 300_000])),) for _ in range(T)]
+        dtypes = [torch.float32 if rng.random() < 0.9 else torch.int64 for _ in range(T)]
+        L = BucketLayout([f"t{i}" for i in range(T)], shapes, dtypes)
+        segs = PieceSegments(L, min_bytes=4 * 70_000)
+        pos = 0
+        for off, n, k in segs.segs:
+            assert off == pos and n > 0
+            pos += n
+        assert pos == L.P_full
+        large = [e for e in L.f_entries if e.numel >= 70_000]
+        assert [segs.segs[i][1] for i in range(len(segs.segs)) if segs.segs[i][2] >= 0] == [e.numel for e in large]
+        assert len(segs.large_pieces) + len(segs.small_pieces) == sum(1 for e in L.f_entries if e.numel)
+        for N in (1, 2, 3, 8):
+            S = (-(-max(1, L.P_full) // N) + 63) // 64 * 64  # BucketLayout's shard
+            for r in range(N):
+                p0, p1 = min(L.P_full, r * S), min(L.P_full, (r + 1) * S)
+                dst, nb, kind, soff = segs.part_plan(p0, p1)
+                got = sum(int(b) for b in nb)
+                assert got == 4 * (p1 - p0)
+                cur = 0
+                for d, b in zip(dst.tolist(), nb.tolist()):
+                    assert d == cur and b > 0
+                    cur += b

@@ -13,6 +13,6 @@ for spec in "$@"; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -DFA_TUNING=1 \
     -DQF_KERNEL=$KK -DQF_CHAIN_KERNEL=$CK -DQF2_V=$V -DQF2_WAVES=$W -DQF2_GRID=$G -DQF_PLAIN_GLDS=$GL -DQF_CHAIN_GLDS=$GL -DQF_EMAX=$EM -DQF_PART=$PT -DQF_WIDE_BYTES=${WB}LL \
     -o $out $ROOT/fedscale_amd/csrc/fedagg.hip $ROOT/fedscale_amd/csrc/client_update.hip \
-    $ROOT/fedscale_amd/csrc/ingress_host.cpp $ROOT/fedscale_amd/csrc/rccl_comm.cpp &
+    $ROOT/fedscale_amd/csrc/ingress_host.cpp $ROOT/fedscale_amd/csrc/ingress_dma.cpp $ROOT/fedscale_amd/csrc/rccl_comm.cpp &
 done
 wait

@@ -11,7 +11,7 @@ for spec in "$@"; do
   defs=${spec#*=}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -ffp-contract=off -DFA_TUNING=1 $defs \
     -o $ROOT/fedscale_amd/variants/libfedagg_qf2_$name.so $ROOT/fedscale_amd/csrc/fedagg.hip \
-    $ROOT/fedscale_amd/csrc/client_update.hip $ROOT/fedscale_amd/csrc/ingress_host.cpp \
+    $ROOT/fedscale_amd/csrc/client_update.hip $ROOT/fedscale_amd/csrc/ingress_host.cpp $ROOT/fedscale_amd/csrc/ingress_dma.cpp \
     $ROOT/fedscale_amd/csrc/rccl_comm.cpp &
 done
 wait

@@ -4,6 +4,7 @@
 #   tune5    q-FedAvg chain-grid variants (fedscale_amd/variants, tools/build_qf_defs.sh), interleaved:
 #            config 5's shard chunk (1024 x 12.5 M, first and later passes) and 1000 x 25 M
 #   reg      N-GPU ingress: gather into a pinned row vs hipHostRegister of the payload (tools/register_probe.py)
+#   sreg     the same through ShardedModelAdapter (RegisteredUpload vs the pinned-row gather), 1/2/4 parts
 #   bench    default bench line (all configs)
 #   c4       config 4 as the drop-in runs it (mean, then k_yogi_step): kernel trace + stats
 #   c5       config 5's shard of 8: kernel trace + stats, FETCH_SIZE / WRITE_SIZE (MI355X_MICROARCH.md recipe)
@@ -34,6 +35,11 @@ reg)
   for L in p25m resnet18; do
     timeout -k 10 300 python -u tools/register_probe.py $L 1,2,4 16 > $OUT/${T}_register_$L.log 2>&1 || { tail -20 $OUT/${T}_register_$L.log; exit 1; }
     cat $OUT/${T}_register_$L.log
+  done ;;
+sreg)
+  for L in p25m resnet18; do
+    timeout -k 10 400 python -u tools/sharded_ingress_bench.py 24 3 $L 1,2,4 payload > $OUT/${T}_sharded_ingress_$L.log 2>&1 || { tail -20 $OUT/${T}_sharded_ingress_$L.log; exit 1; }
+    grep '^{' $OUT/${T}_sharded_ingress_$L.log
   done ;;
 bench)
   timeout -k 10 700 python -u bench.py > $OUT/${T}_bench.log 2>&1 || { tail -20 $OUT/${T}_bench.log; exit 1; }
