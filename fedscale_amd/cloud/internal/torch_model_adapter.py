@@ -313,10 +313,30 @@ class TorchModelAdapter(ModelAdapterBase):
             if snap.readers == 0 and snap is not self._snap:
                 self._snap_pool.append(snap.buf)
 
+    #: models of at least this many bytes clone the snapshot with the native multi-threaded copy (fa_host_gather):
+    #: one memcpy stream moves ~10 GB/s, so get_weights() of the headline's 100 MB model spent 10 of its 13 ms on
+    #: the clones (bench.py headline_model_pcie_inclusive, phases_ms)
+    CLONE_PARALLEL_MIN_BYTES = 16 << 20
+
     def _clone_weights(self, snap: "_HostSnapshot") -> list:
         # the reference's params.data.clone() per entry (torch_model_adapter.py:47): a fresh CPU tensor each,
         # copied through numpy (half the per-tensor cost of Tensor.clone on small models)
-        return [torch.from_numpy(a.copy()) for a in snap.buf.np_views]
+        views = snap.buf.np_views
+        if self.layout.P_full * 4 < self.CLONE_PARALLEL_MIN_BYTES:
+            return [torch.from_numpy(a.copy()) for a in views]
+        from ... import _native
+        from ...bucket import default_pack_workers
+
+        outs = [np.empty(a.shape, dtype=a.dtype) for a in views]  # independent tensors, as clone() returns
+        off = np.zeros(1, dtype=np.int64)
+        workers = default_pack_workers()
+        for a, o in zip(views, outs):  # one multi-threaded copy per entry (small ones stay one memcpy in C)
+            if a.nbytes:
+                sp = np.asarray([a.__array_interface__["data"][0]], dtype=np.uint64)
+                nn = np.asarray([a.nbytes], dtype=np.int64)
+                _native.call("fa_host_gather", o.__array_interface__["data"][0], sp.ctypes.data, off.ctypes.data,
+                             nn.ctypes.data, 1, workers)
+        return [torch.from_numpy(o) for o in outs]
 
     def get_weights(self) -> List[torch.Tensor]:
         """torch_model_adapter.py:41-47: cloned CPU tensors in state_dict order (gathers the shards).

@@ -259,3 +259,32 @@ def test_zero_copy_payload_ingress_matches_reference(gpu_device, name, monkeypat
             assert_state_close(got, sc.expected(r), 1e-5, f"{name} r{r}")
         else:
             assert_state_equal(got, sc.expected(r), f"{name} r{r}")
+
+
+def test_get_weights_of_a_large_model_clones_in_parallel(gpu_device):
+    """get_weights() of a model above CLONE_PARALLEL_MIN_BYTES clones the host snapshot with the native
+    multi-threaded copy: the same values as the reference's per-entry clone (torch_model_adapter.py:41-47), each
+    entry its own tensor, and writing to one returned tensor changes neither the snapshot nor the next call."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+    from oracle.cpu_reference import fedavg_close, fedavg_step
+    from tests.golden_io import StateDictModule
+
+    names = ["w0", "w1", "tiny"]
+    init = [torch.zeros(3_000_000), torch.zeros(2000, 1001), torch.zeros(3)]
+    ad = TorchModelAdapter(StateDictModule(names, init), device="cuda:0")
+    assert ad.layout.P_full * 4 >= ad.CLONE_PARALLEL_MIN_BYTES
+    agg = DeviceAggregator(ad)
+    rng = np.random.default_rng(4)
+    acc = None
+    agg.start_round(3)
+    for k in range(3):
+        up = [rng.standard_normal(tuple(t.shape)).astype(np.float32) for t in init]
+        acc = fedavg_step(acc, up, k == 0)
+        agg.on_result({"client_id": k, "update_weight": up, "moving_loss": 1.0})
+    want = fedavg_close(acc, 3)
+    got = ad.get_weights()
+    assert_state_equal(got, want, "parallel clone")
+    assert len({t.data_ptr() for t in got}) == len(got)
+    got[0].fill_(7.0)
+    assert_state_equal(ad.get_weights(), want, "a second call after the caller wrote into the first list")
