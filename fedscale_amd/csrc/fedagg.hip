@@ -790,7 +790,10 @@ static inline int qf_grid(bool chain) { return chain ? QF_CHAIN_GRID : QF_GRID; 
 #ifndef QF_BALANCE
 #define QF_BALANCE 1  // 0: always full-width tiles (plain grid-stride)
 #endif
+#ifndef QF_MAXK
 #define QF_MAXK 1024  // LDS: 4 waves x 1024 clients x 8 B = 32 KiB per workgroup
+#endif
+static_assert(QF_MAXK % 4 == 0 && QF_MAXK <= 4096, "QF_MAXK: a multiple of 4, <= 4096 (LDS)");
 
 struct QfArgs {
   const float* x;

@@ -11,10 +11,26 @@
 #include <stdint.h>
 #include <stdio.h>
 
+#include <mutex>
 #include <vector>
 
 #include "../../include/fedagg.h"
 #include "fa_device.h"
+
+namespace {
+// The ranges registered through fa_host_register: hipMemGetAddressRange does not report registered host memory,
+// so fa_h2d_pieces checks a piece's source extent against this list (pinned hipHostMalloc memory it asks HIP).
+std::mutex g_reg_mu;
+std::vector<std::pair<uintptr_t, uintptr_t>> g_regs;
+
+bool registered(const void* p, uint64_t n) {
+  const uintptr_t a = (uintptr_t)p;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (const auto& r : g_regs)
+    if (a >= r.first && a < r.second) return n <= r.second - a;
+  return false;
+}
+}  // namespace
 
 extern "C" int fa_host_register(void* p, int64_t nbytes) {
   if (!p || nbytes <= 0) return fa_internal_set_error(FA_E_ARG, "fa_host_register: NULL pointer or empty range");
@@ -26,11 +42,21 @@ extern "C" int fa_host_register(void* p, int64_t nbytes) {
              hipGetErrorString(e));
     return fa_internal_set_error(FA_E_HIP, buf);
   }
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  g_regs.emplace_back((uintptr_t)p, (uintptr_t)p + (uintptr_t)nbytes);
   return FA_OK;
 }
 
 extern "C" int fa_host_unregister(void* p) {
   if (!p) return FA_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    for (size_t i = 0; i < g_regs.size(); ++i)
+      if (g_regs[i].first == (uintptr_t)p) {
+        g_regs.erase(g_regs.begin() + (long)i);
+        break;
+      }
+  }
   const hipError_t e = hipHostUnregister(p);
   if (e != hipSuccess) {
     (void)hipGetLastError();
@@ -56,7 +82,8 @@ extern "C" int fa_h2d_pieces(void* const* dst, const void* const* src, const int
     for (int i = 0; i < n; ++i) {
       if (sidx[i] != s || nbytes[i] == 0) continue;
       FA_OPERAND("dst", dst[i], (uint64_t)nbytes[i]);
-      const int e = fa_scope_.host_source("src", src[i], (uint64_t)nbytes[i]);
+      if (registered(src[i], (uint64_t)nbytes[i])) continue;  // inside one of our registrations
+      const int e = fa_scope_.host_source("src", src[i], (uint64_t)nbytes[i]);  // else: pinned memory
       if (e) return e;
     }
   }

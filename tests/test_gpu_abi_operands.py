@@ -193,7 +193,8 @@ def test_pageable_operand_in_every_position_is_rejected_before_any_launch(gpu_de
     # every launching entry point of the ABI is covered (queries, host-only and RCCL calls are not launches)
     host_or_query = {"fa_abi_version", "fa_last_error_string", "fa_pointer_kind", "fa_reduce_launches",
                      "fa_qfed_launches", "fa_qfed_max_chunk", "fa_qfed_workspace_bytes", "fa_host_gather",
-                     "fa_pickle_strip", "fa_dp_workspace_bytes"}
+                     "fa_pickle_strip", "fa_dp_workspace_bytes", "fa_host_register", "fa_host_unregister",
+                     "fa_h2d_pieces"}  # (fa_h2d_pieces: its own test below)
     rccl = {n for n in exported if n.startswith("fa_rccl_")}
     assert exported - host_or_query - rccl == {c.name for c in cases}
 
@@ -285,3 +286,48 @@ def test_rccl_buffers_are_checked(gpu_device):
         assert torch.equal(recv, send)
     finally:
         N.call("fa_rccl_destroy", comm)
+
+
+def test_h2d_pieces_checks_every_piece(gpu_device):
+    """fa_h2d_pieces (round-4 N-GPU ingress): a source must be registered (fa_host_register, checked against the
+    library's own list of registrations, extent included) or pinned host memory, a destination device memory of its
+    stream's device holding the piece; a bad piece anywhere refuses the whole call before any copy is enqueued."""
+    from fedscale_amd import _native as N
+
+    lib = N.load()
+    st = torch.cuda.current_stream().cuda_stream
+    host = np.arange(1 << 18, dtype=np.float32)  # pageable until registered
+    pinned = torch.arange(1 << 10, dtype=torch.float32).pin_memory()
+    dst = torch.zeros(1 << 18, device=gpu_device)
+    streams = _u64([st])
+
+    def call(pieces):
+        d = _u64([p[0] for p in pieces])
+        s = _u64([p[1] for p in pieces])
+        nb = np.asarray([p[2] for p in pieces], dtype=np.int64)
+        si = np.zeros(len(pieces), dtype=np.int32)
+        rc = lib.fa_h2d_pieces(d.ctypes.data, s.ctypes.data, nb.ctypes.data, si.ctypes.data, len(pieces),
+                               streams.ctypes.data, 1)
+        return rc, lib.fa_last_error_string().decode()
+
+    half = host.nbytes // 2
+    good = (dst.data_ptr(), pinned.data_ptr(), pinned.numel() * 4)
+    rc, msg = call([good, (dst.data_ptr() + 4096, host.ctypes.data, half)])
+    assert rc == -1 and "src" in msg and "not registered" in msg, msg
+    torch.cuda.synchronize()
+    assert int(torch.count_nonzero(dst)) == 0  # the good piece before it was not copied either
+    N.call("fa_host_register", host.ctypes.data, host.nbytes)
+    try:
+        rc, msg = call([good, (dst.data_ptr() + 4096, host.ctypes.data + half, half + 4)])
+        assert rc == -1 and "src" in msg, msg  # 4 bytes past the registration
+        rc, msg = call([(host.ctypes.data, pinned.data_ptr(), 64)])
+        assert rc == -1 and "dst" in msg, msg
+        rc, msg = call([good, (dst.data_ptr() + pinned.numel() * 4, host.ctypes.data + 4096, half)])
+        assert rc == 0, msg
+        torch.cuda.synchronize()
+        want = np.concatenate([pinned.numpy(), host[1024:1024 + half // 4]])
+        np.testing.assert_array_equal(dst[:want.size].cpu().numpy(), want)
+    finally:
+        N.call("fa_host_unregister", host.ctypes.data)
+    rc, msg = call([(dst.data_ptr(), host.ctypes.data, 64)])  # released: no longer a valid source
+    assert rc == -1, msg
