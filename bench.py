@@ -274,7 +274,10 @@ def c1_host_round(dev, seed: int, rounds: int = 300) -> dict:
             "job_config": {"file": "benchmark/configs/femnist/conf.yml (job_conf)",
                            "num_participants": f"{job['job_conf_num_participants']} -> {K}",
                            "gradient_policy": args.gradient_policy, "learning_rate": args.learning_rate,
-                           "local_steps": args.local_steps, "data_set": args.data_set},
+                           "local_steps": args.local_steps, "data_set": args.data_set,
+                           "model": (f"the job config names {args.model!r} (conf.yml:40); this line uses BASELINE "
+                                     "config 1's FEMNIST small-CNN layout (MnistCNN with a 62-way head, P = 24,492, "
+                                     "SURVEY §8) as BASELINE.json names it — the ResNet-18 layout is config 3")},
             "note": "host dicts in, global model out (get_weights); median of %d rounds" % rounds}
 
 

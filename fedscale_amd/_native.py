@@ -39,6 +39,8 @@ SIGNATURES = {
     "fa_reduce_mirror": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32, _i32,
                                 _c_void_p]),
     "fa_reduce_launches": (_i64, [_i32, _i64, _i32]),
+    "fa_reduce_parts": (_i32, [_i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32, _c_void_p,
+                               _c_void_p]),
     "fa_qfed_launches": (_i64, [_i64, _i64, _i32]),
     "fa_reduce_yogi": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p,
                               _c_void_p, _c_void_p, _c_void_p, _f32, _f32, _f32, _f32, _f32, _i32, _c_void_p]),

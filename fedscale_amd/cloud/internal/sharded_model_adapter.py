@@ -229,11 +229,49 @@ class ShardedModelAdapter(TorchModelAdapter):
                     keep_mean: bool = True):
         if rnd.policy == "qfedavg":
             self._apply_qfed(rnd)
-        else:
+        elif not self._finish_parts_at_once(rnd, denom32, denom64):
             for p, r in zip(self.parts, rnd.rounds):
                 p.apply_round(r, denom32, denom64, None, keep_mean)
         self._commit()
         self._release_registrations(block=False)
+
+    #: FedAvg rounds without a server step finish every part with ONE native call (fa_reduce_parts)
+    FINISH_PARTS_AT_ONCE = True
+
+    def _finish_parts_at_once(self, rnd: ShardedRound, denom32: float, denom64: float) -> bool:
+        """FedAvg without a server step (the mean IS the new model, aggregator.py:505-511): every part's finishing
+        reduce goes out in one native call instead of one Python call chain per part — the same launches on the
+        same streams, so the same bits; the per-part host cost was the in-process round's serial part.  The side
+        table and the version commit follow per part.  False: take the per-part path (other policies, a server
+        optimizer, one part)."""
+        from ... import kernels as kx
+
+        opt = self.optimizer
+        if (not self.FINISH_PARTS_AT_ONCE or rnd.policy != "fedavg" or len(self.parts) < 2
+                or (opt is not None and getattr(opt, "mode", None) in ("fed-yogi", "q-fedavg"))
+                or any(r.cg is not None for r in rnd.rounds)):
+            return False
+        xs, Ks, Ps, outs, accs, sides = [], [], [], [], [], []
+        for p, r in zip(self.parts, rnd.rounds):
+            r._check_complete()
+            r.staging.drain()
+            out_f, out_s = p._scratch_buffers()
+            xs.append(r.staging.x)
+            Ks.append(r.slot)
+            Ps.append(p.layout.P)
+            outs.append(out_f)
+            accs.append(None if r.chunks_done == 0 else r.acc)
+            sides.append(out_s)
+        kx.reduce_parts(xs, Ks, Ps, outs, accs, [p.dstream.handle for p in self.parts], denom=denom32, finalize=True)
+        for p, r, out_f, out_s in zip(self.parts, rnd.rounds, outs, sides):
+            with p.dstream.joined():  # the caller's stream on this GPU is ordered after the part's work
+                L = p.layout
+                kx.side_accumulate(r.staging.xi, r.slot, L.Q, 0, acc_i=r.acc_i, acc_d=r.acc_d,
+                                   accumulate=r.chunks_done > 0)
+                kx.side_close(L.Q, 0, denom64, acc_i=r.acc_i, acc_d=r.acc_d, cur=p._mean_s, model=out_s)
+                p._mean_f, p._mean_valid = out_f, True
+                p._commit_scratch()
+        return True
 
     def _apply_qfed(self, rnd: ShardedRound):
         mode = getattr(self.optimizer, "mode", None)

@@ -665,6 +665,40 @@ extern "C" int fa_reduce(const float* x, int64_t ld, int32_t K, int64_t P, const
   return launch_reduce<EPI_CHAIN>(r, st, "fa_reduce");
 }
 
+// The finishing reduce of every part of a model sharded over the GPUs of this process, in one call (round 4): the
+// in-process N-GPU round's host cost per part drops from a Python call chain to a DevScope and the plan's launches.
+// Every part is validated (sizes, stream, operands) before any part launches.
+extern "C" int fa_reduce_parts(int32_t n, const float* const* x, const int64_t* ld, const int32_t* K,
+                               const int64_t* P, const float* const* acc_in, float* const* out, float denom,
+                               const int32_t* flags, void* const* streams) {
+  if (n < 1 || !x || !ld || !K || !P || !acc_in || !out || !flags || !streams)
+    return fail(FA_E_ARG, "fa_reduce_parts: NULL table or n < 1");
+  char what[48];
+  for (int i = 0; i < n; ++i) {
+    snprintf(what, sizeof(what), "fa_reduce_parts[%d]", i);
+    int e = check_reduce_args(what, x[i], ld[i], K[i], P[i], acc_in[i], out[i], flags[i]);
+    if (e) return e;
+    if (!streams[i]) return fail(FA_E_ARG, "%s: NULL stream (one stream per part's GPU)", what);
+    if (P[i] == 0) continue;
+    FA_DEVICE_SCOPE(what, streams[i], out[i]);
+    FA_OPERAND("x", x[i], rows_bytes(K[i], ld[i], P[i]));
+    FA_OPERAND("acc_in", (flags[i] & FA_ACCUMULATE) ? acc_in[i] : nullptr, cols_bytes(P[i]));
+    FA_OPERAND("out", out[i], cols_bytes(P[i]));
+  }
+  for (int i = 0; i < n; ++i) {
+    if (P[i] == 0) continue;
+    snprintf(what, sizeof(what), "fa_reduce_parts[%d]", i);
+    RedArgs r{};
+    r.x = x[i]; r.ld4 = ld[i] / 4; r.P4 = (P[i] + 3) / 4; r.K = K[i]; r.flags = flags[i]; r.acc_in = acc_in[i];
+    r.out = out[i]; r.denom = denom;
+    FA_DEVICE_SCOPE(what, streams[i], out[i]);
+    const int e = (flags[i] & FA_FINALIZE) ? launch_reduce<EPI_MEAN>(r, (hipStream_t)streams[i], what)
+                                           : launch_reduce<EPI_CHAIN>(r, (hipStream_t)streams[i], what);
+    if (e) return e;
+  }
+  return FA_OK;
+}
+
 extern "C" int fa_reduce_mirror(const float* x, int64_t ld, int32_t K, int64_t P, const float* a,
                                 const float* acc_in, float* out, float* mirror, float denom, int32_t flags,
                                 fa_stream_t stream) {

@@ -80,6 +80,31 @@ def reduce(x: torch.Tensor, K: int, P: int, out: torch.Tensor, *, a: Optional[to
     return out
 
 
+def reduce_parts(xs, Ks, Ps, outs, acc_ins, streams, *, denom: float, finalize: bool):
+    """fa_reduce over every part of a model sharded over this process's GPUs, in one native call (unweighted):
+    part i reduces xs[i][:Ks[i], :Ps[i]] (continuing acc_ins[i] when not None) into outs[i] on streams[i] (a
+    hipStream_t of that part's GPU).  The library checks every part's stream and operands before launching."""
+    import numpy as np
+
+    n = len(xs)
+    for name, seq in (("x", xs), ("out", outs)):
+        for t in seq:
+            if t.dtype != torch.float32 or not t.is_contiguous() or t.device.type != "cuda":
+                raise ValueError(f"reduce_parts: {name} must be contiguous float32 device tensors")
+    ptrs = lambda ts: np.asarray([0 if t is None else t.data_ptr() for t in ts], dtype=np.uint64)  # noqa: E731
+    x_t, o_t, a_t = ptrs(xs), ptrs(outs), ptrs(acc_ins)
+    ld = np.asarray([t.shape[-1] for t in xs], dtype=np.int64)
+    K = np.asarray(Ks, dtype=np.int32)
+    P = np.asarray(Ps, dtype=np.int64)
+    fl = np.asarray([(FA_ACCUMULATE if a is not None else 0) | (FA_FINALIZE if finalize else 0) for a in acc_ins],
+                    dtype=np.int32)
+    import ctypes
+
+    st = (ctypes.c_void_p * n)(*streams)  # a per-part stream table (as the fa_rccl_* calls take it)
+    call("fa_reduce_parts", n, x_t.ctypes.data, ld.ctypes.data, K.ctypes.data, P.ctypes.data, a_t.ctypes.data,
+         o_t.ctypes.data, float(denom), fl.ctypes.data, st)
+
+
 def reduce_mirror(x: torch.Tensor, K: int, P: int, out: torch.Tensor, mirror: torch.Tensor, *,
                   a: Optional[torch.Tensor] = None, acc_in: Optional[torch.Tensor] = None,
                   denom: float = 1.0) -> torch.Tensor:

@@ -78,6 +78,18 @@ int fa_reduce(const float* x, int64_t ld, int32_t K, int64_t P, const float* a, 
               float* out, float denom, int32_t flags, fa_stream_t stream);
 
 /*
+ * fa_reduce for every part of a model sharded over the GPUs of ONE process (ShardedModelAdapter), in one call:
+ * part i reduces x[i] (K[i] rows of ld[i] floats, P[i] columns) into out[i] (continuing acc_in[i] with
+ * FA_ACCUMULATE) on streams[i], a stream of the GPU holding out[i] (never NULL), with fa_reduce's arithmetic,
+ * denom and flags[i]; unweighted (FedAvg).  Every part is checked before any part launches.  Replaces the same
+ * lines as fa_reduce (aggregator.py:497-507) for the finish of an in-process N-GPU round (the per-part host call
+ * chain was the round's serial part: DESIGN.md §6).
+ */
+int fa_reduce_parts(int32_t n, const float* const* x, const int64_t* ld, const int32_t* K, const int64_t* P,
+                    const float* const* acc_in, float* const* out, float denom, const int32_t* flags,
+                    fa_stream_t const* streams);
+
+/*
  * fa_reduce with FA_FINALIZE whose epilogue writes the mean twice: into out (device, the new global model)
  * and into `mirror` (round_up(P, 4) floats), which may be PINNED HOST memory (page-locked, mapped for the
  * GPU of `out`).  `x` may be pinned host memory too: the kernel then reads the client rows over PCIe.

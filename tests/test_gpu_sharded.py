@@ -119,7 +119,9 @@ def test_sharded_equals_single_gpu(gpu_device, name):
 LAUNCHES = {"fa_reduce", "fa_reduce_mirror", "fa_reduce_yogi", "fa_yogi_step", "fa_qfed_accumulate", "fa_qfed_hs", "fa_qfed_finalize",
             "fa_sum_rows_f64", "fa_side_accumulate", "fa_side_close", "fa_side_yogi", "fa_side_qfed_accumulate",
             "fa_side_qfed_finalize", "fa_fill_synthetic", "fa_prefix_box_combine", "fa_rccl_all_gather",
-            "fa_rccl_all_reduce", "fa_rccl_gather", "fa_rccl_broadcast"}
+            "fa_rccl_all_reduce", "fa_rccl_gather", "fa_rccl_broadcast", "fa_reduce_parts"}
+#: ... of them, those that take a per-part stream table (one stream per position of the adapter's group)
+TABLE_LAUNCHES = {"fa_rccl_all_gather", "fa_rccl_all_reduce", "fa_rccl_gather", "fa_rccl_broadcast", "fa_reduce_parts"}
 
 
 def _spy_native(monkeypatch):
@@ -145,7 +147,7 @@ def _check_part_streams(calls, adapter, ctx):
     launches = [c for c in calls if c[0] in LAUNCHES]
     assert launches, ctx
     for fn, st, cur in launches:
-        if fn.startswith("fa_rccl_"):
+        if fn in TABLE_LAUNCHES:
             hs = list(st)
             assert hs == adapter.group.stream_handles() and all(hs), f"{ctx}: {fn} stream table {hs}"
             continue
@@ -185,7 +187,8 @@ def test_every_native_call_runs_on_its_parts_stream(gpu_device, monkeypatch, nam
         _check(sc, r, adapter.get_weights(), adapter, f"{name} {sharding} r{r}")
         list(agg.model_weights)  # the FedAvg mean's D2H runs on the parts' streams too
     launches = _check_part_streams(calls, adapter, f"{name} {sharding}")
-    used = {c[1] for c in launches if not c[0].startswith("fa_rccl_")}
+    used = {c[1] for c in launches if c[0] not in TABLE_LAUNCHES}
+    used |= {h for c in launches if c[0] == "fa_reduce_parts" for h in c[1]}
     assert used == set(adapter.group.stream_handles()), "every part launched on its own stream"
     if sc.meta["policy"] == "q-fedavg":
         assert any(c[0] in ("fa_rccl_all_gather", "fa_sum_rows_f64") for c in launches)
