@@ -681,9 +681,13 @@ extern "C" int fa_reduce_parts(int32_t n, const float* const* x, const int64_t* 
     if (!streams[i]) return fail(FA_E_ARG, "%s: NULL stream (one stream per part's GPU)", what);
     if (P[i] == 0) continue;
     FA_DEVICE_SCOPE(what, streams[i], out[i]);
-    FA_OPERAND("x", x[i], rows_bytes(K[i], ld[i], P[i]));
-    FA_OPERAND("acc_in", (flags[i] & FA_ACCUMULATE) ? acc_in[i] : nullptr, cols_bytes(P[i]));
-    FA_OPERAND("out", out[i], cols_bytes(P[i]));
+    char nx[24], na[24], no[24];
+    snprintf(nx, sizeof(nx), "x[%d]", i);
+    snprintf(na, sizeof(na), "acc_in[%d]", i);
+    snprintf(no, sizeof(no), "out[%d]", i);
+    FA_OPERAND(nx, x[i], rows_bytes(K[i], ld[i], P[i]));
+    FA_OPERAND(na, (flags[i] & FA_ACCUMULATE) ? acc_in[i] : nullptr, cols_bytes(P[i]));
+    FA_OPERAND(no, out[i], cols_bytes(P[i]));
   }
   for (int i = 0; i < n; ++i) {
     if (P[i] == 0) continue;

@@ -108,6 +108,12 @@ def _cases(dev, st):
              lambda p: (p["xs"], p["desc"], K, p["tensors"], 1, p["chunk_tensor"], p["chunk_first"], 1, p["global"],
                         st)),
         Case("fa_dp_normals", dict(out=f(64)), ["out"], lambda p: (p["out"], 64, 5, 0, st)),
+        # the in-process N-GPU finish: two parts (on the one card), tables of per-part operands
+        Case("fa_reduce_parts", {"x": [f(K * LD, 0.5), f(K * LD, 0.25)], "acc_in": [f(LD, 0.0), f(LD, 0.0)],
+                                 "out": [f(LD), f(LD)]}, ["out"],
+             lambda p: (2, t(p["x"]), host(np.int64, [LD, LD]), host(np.int32, [K, K]), host(np.int64, [P, P]),
+                        t(p["acc_in"]), t(p["out"]), ctypes.c_float(4.0), host(np.int32, [FIN | ACC] * 2),
+                        t([st, st]))),
         # client-side pointer tables (include/fedclient.h)
         Case("fa_prox_update", {"param": tab(1.0), "global": tab(2.0)}, ["param"],
              lambda p: (t(p["param"]), t(p["global"]), numel.ctypes.data, 2, ctypes.c_float(0.1), st)),
