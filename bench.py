@@ -746,7 +746,7 @@ def run_inproc_bench(world: int, K: int, P: int, backend: str, timeout_s: int = 
     nd = torch.cuda.device_count()
     devs = [i % max(1, nd) for i in range(world)]
     cmd = [sys.executable, "-m", "fedscale_amd.inproc_bench", "--devices", ",".join(map(str, devs)),
-           "--clients", str(K), "--params", str(P)]
+           "--clients", str(K), "--params", str(P), "--policies", "fedavg,fed-yogi"]
     t0 = time.perf_counter()
     try:
         r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout_s)
@@ -757,7 +757,8 @@ def run_inproc_bench(world: int, K: int, P: int, backend: str, timeout_s: int = 
         return {"devices": devs, "ok": False, "rc": r.returncode, "error": r.stderr[-400:]}
     rep = json.loads(lines[-1])
     rep["seconds"] = round(time.perf_counter() - t0, 1)
-    if not rep.get("distinct_gpus", True):
+    rep["workloads"] = "fedavg: the headline round; fed-yogi: config 4's (1000 x 25 M, mean then YoGi step per part)"
+    if len(set(devs)) < len(devs):
         rep["note"] = (f"{world} parts on {len(set(devs))} GPU(s) (backend {backend} rehearsal): plumbing only, "
                        "not an N-GPU rate")
     return rep

@@ -35,6 +35,19 @@ def _model(P: int, seed: int):
     return synth.LayoutModule(names, shapes, [torch.float32] * n, seed=seed)
 
 
+def _optimizer(policy: str, device):
+    """The server optimizer of the round (None for FedAvg): FedYoGi is config 4's server step (optimizers.py:43-63)."""
+    if policy == "fedavg":
+        return None
+    import argparse
+
+    from .cloud.aggregation.optimizers import TorchServerOptimizer
+
+    args = argparse.Namespace(gradient_policy=policy, yogi_eta=3e-3, yogi_tau=1e-8, yogi_beta=0.9, yogi_beta2=0.99,
+                              learning_rate=0.05, qfed_q=1.0)
+    return TorchServerOptimizer(policy, args, device)
+
+
 def _time_rounds(adapter, parts_streams, K: int, rounds: int, warmup: int) -> dict:
     """Warmup, then ``rounds`` timed rounds; per-part event pairs on each part's stream."""
     import numpy as np
@@ -90,7 +103,9 @@ def _time_rounds(adapter, parts_streams, K: int, rounds: int, warmup: int) -> di
 
 
 def run(devices, K: int = 1000, P: int = 25_000_000, rounds: int = 6, warmup: int = 2, seed: int = 2024,
-        one_gpu: bool = True) -> dict:
+        one_gpu: bool = True, policy: str = "fedavg") -> dict:
+    """``policy``: "fedavg" (the headline) or "fed-yogi" (config 4: the mean, then the YoGi step on every part).
+    A round's arrivals are FedAvg arrivals either way; the server optimizer decides the finish."""
     import torch
 
     from . import synth
@@ -98,10 +113,11 @@ def run(devices, K: int = 1000, P: int = 25_000_000, rounds: int = 6, warmup: in
     from .cloud.internal.torch_model_adapter import TorchModelAdapter
 
     N = len(devices)
-    out = {"devices": list(devices), "clients": K, "params": P, "policy": "fedavg",
+    out = {"devices": list(devices), "clients": K, "params": P, "policy": policy,
            "distinct_gpus": len(set(devices)) == N}
-    alg = 4 * K * P + 4 * P
-    ad = ShardedModelAdapter(_model(P, seed), devices=list(devices), staging_capacity=K)
+    alg = 4 * K * P + (4 * P if policy == "fedavg" else 24 * P)
+    ad = ShardedModelAdapter(_model(P, seed), optimizer=_optimizer(policy, devices[0]), devices=list(devices),
+                             staging_capacity=K)
     try:
         out["transport"] = ad.group.transport
         rnd = ad.begin_round(K, "fedavg", capacity=K)
@@ -122,7 +138,7 @@ def run(devices, K: int = 1000, P: int = 25_000_000, rounds: int = 6, warmup: in
                 torch.cuda.empty_cache()
     if one_gpu:
         d0 = devices[0]
-        one = TorchModelAdapter(_model(P, seed), device=d0, staging_capacity=K)
+        one = TorchModelAdapter(_model(P, seed), optimizer=_optimizer(policy, d0), device=d0, staging_capacity=K)
         rnd = one.begin_round(K, "fedavg", capacity=K)
         with one.dstream:
             synth.fill(rnd.staging.x, K, P, seed=seed)
@@ -146,13 +162,18 @@ def main(argv=None):
     p.add_argument("--params", type=int, default=25_000_000)
     p.add_argument("--rounds", type=int, default=6)
     p.add_argument("--no-one-gpu", action="store_true")
+    p.add_argument("--policies", default="fedavg", help="comma-separated: fedavg, fed-yogi")
     a = p.parse_args(argv)
     devices = [int(d) for d in a.devices.split(",") if d.strip()]
-    try:
-        rep = run(devices, K=a.clients, P=a.params, rounds=a.rounds, one_gpu=not a.no_one_gpu)
-        rep["ok"] = True
-    except Exception as e:  # reported, not raised: bench.py records the failure
-        rep = {"devices": devices, "ok": False, "error": f"{type(e).__name__}: {e}"}
+    reps = {}
+    for pol in [x.strip() for x in a.policies.split(",") if x.strip()]:
+        try:
+            r = run(devices, K=a.clients, P=a.params, rounds=a.rounds, one_gpu=not a.no_one_gpu, policy=pol)
+            r["ok"] = True
+        except Exception as e:  # reported, not raised: bench.py records the failure
+            r = {"devices": devices, "policy": pol, "ok": False, "error": f"{type(e).__name__}: {e}"}
+        reps[pol] = r
+    rep = reps[next(iter(reps))] if len(reps) == 1 else {"ok": all(r["ok"] for r in reps.values()), "policies": reps}
     print(json.dumps(rep), flush=True)
     return 0 if rep.get("ok") else 1
 
