@@ -46,6 +46,8 @@ SIGNATURES = {
                               _c_void_p, _c_void_p, _c_void_p, _f32, _f32, _f32, _f32, _f32, _i32, _c_void_p]),
     "fa_yogi_step": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i64, _f32, _f32, _f32, _f32,
                             _f32, _i32, _c_void_p]),
+    "fa_yogi_step_parts": (_i32, [_i32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32, _f32,
+                                  _f32, _f32, _f32, _i32, _c_void_p]),
     "fa_qfed_max_chunk": (_i32, []),
     "fa_qfed_workspace_bytes": (_i64, [_i32, _i64, _i64]),
     "fa_qfed_accumulate": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _f32, _c_void_p, _c_void_p,

@@ -235,41 +235,70 @@ class ShardedModelAdapter(TorchModelAdapter):
         self._commit()
         self._release_registrations(block=False)
 
-    #: FedAvg rounds without a server step finish every part with ONE native call (fa_reduce_parts)
+    #: FedAvg rounds (without a server step, or with FedYoGi's) finish every part with ONE native call per pass
+    #: (fa_reduce_parts, then fa_yogi_step_parts)
     FINISH_PARTS_AT_ONCE = True
 
     def _finish_parts_at_once(self, rnd: ShardedRound, denom32: float, denom64: float) -> bool:
-        """FedAvg without a server step (the mean IS the new model, aggregator.py:505-511): every part's finishing
-        reduce goes out in one native call instead of one Python call chain per part — the same launches on the
-        same streams, so the same bits; the per-part host cost was the in-process round's serial part.  The side
-        table and the version commit follow per part.  False: take the per-part path (other policies, a server
-        optimizer, one part)."""
+        """FedAvg rounds of two or more parts: every part's finishing reduce goes out in one native call instead of
+        one Python call chain per part — the same launches on the same streams, so the same bits; the per-part host
+        cost was the in-process round's serial part.  Without a server step the mean IS the new model
+        (aggregator.py:505-511); with FedYoGi (config 4, optimizers.py:43-63, yogi.py:15-36) the mean goes to its
+        own buffer and one more call steps every part (``TorchModelAdapter._apply_round``'s two-pass finish).  The
+        side table and the version commit follow per part.  False: take the per-part path (q-FedAvg, one part,
+        FedBuff, a per-client round)."""
         from ... import kernels as kx
 
         opt = self.optimizer
+        mode = getattr(opt, "mode", None) if opt is not None else None
         if (not self.FINISH_PARTS_AT_ONCE or rnd.policy != "fedavg" or len(self.parts) < 2
-                or (opt is not None and getattr(opt, "mode", None) in ("fed-yogi", "q-fedavg"))
-                or any(r.cg is not None for r in rnd.rounds)):
+                or mode not in (None, "fed-yogi") or any(r.cg is not None for r in rnd.rounds)):
             return False
-        xs, Ks, Ps, outs, accs, sides = [], [], [], [], [], []
-        for p, r in zip(self.parts, rnd.rounds):
+        yogi = mode == "fed-yogi"
+        ys = [p.optimizer.gradient_controller for p in self.parts] if yogi else None
+        if yogi and len({y.initialized for y in ys}) != 1:
+            return False
+        xs, Ks, Ps, means, accs, lasts, outs = [], [], [], [], [], [], []
+        for i, (p, r) in enumerate(zip(self.parts, rnd.rounds)):
             r._check_complete()
             r.staging.drain()
             out_f, out_s = p._scratch_buffers()
+            mean_f = out_f
+            if yogi:
+                last = p._snapshot()
+                if ys[i].layout is None or p._mean_f is None or p._mean_f is last.f32 or p._mean_f is out_f:
+                    with p.dstream:  # first round: the YoGi state and the mean buffer on the part's device
+                        ys[i].bind(p.layout, p.device)
+                        if p._mean_f is None or p._mean_f is last.f32 or p._mean_f is out_f:
+                            p._mean_f = torch.zeros(p.layout.ld, dtype=torch.float32, device=p.device)
+                mean_f = p._mean_f
+                lasts.append(last)
             xs.append(r.staging.x)
             Ks.append(r.slot)
             Ps.append(p.layout.P)
-            outs.append(out_f)
+            means.append(mean_f)
+            outs.append((out_f, out_s))
             accs.append(None if r.chunks_done == 0 else r.acc)
-            sides.append(out_s)
-        kx.reduce_parts(xs, Ks, Ps, outs, accs, [p.dstream.handle for p in self.parts], denom=denom32, finalize=True)
-        for p, r, out_f, out_s in zip(self.parts, rnd.rounds, outs, sides):
+        streams = [p.dstream.handle for p in self.parts]
+        kx.reduce_parts(xs, Ks, Ps, means, accs, streams, denom=denom32, finalize=True)
+        if yogi:
+            y0 = ys[0]
+            kx.yogi_step_parts(means, [last.f32 for last in lasts], [y.m for y in ys], [y.v for y in ys],
+                               [o[0] for o in outs], Ps, streams, init=not y0.initialized, **y0.fp32_hparams())
+        for i, (p, r) in enumerate(zip(self.parts, rnd.rounds)):
+            out_f, out_s = outs[i]
             with p.dstream.joined():  # the caller's stream on this GPU is ordered after the part's work
                 L = p.layout
                 kx.side_accumulate(r.staging.xi, r.slot, L.Q, 0, acc_i=r.acc_i, acc_d=r.acc_d,
                                    accumulate=r.chunks_done > 0)
-                kx.side_close(L.Q, 0, denom64, acc_i=r.acc_i, acc_d=r.acc_d, cur=p._mean_s, model=out_s)
-                p._mean_f, p._mean_valid = out_f, True
+                kx.side_close(L.Q, 0, denom64, acc_i=r.acc_i, acc_d=r.acc_d, cur=p._mean_s,
+                              model=None if yogi else out_s)
+                if yogi:
+                    ys[i].step_side(p._mean_s, lasts[i].side, model=out_s)
+                    ys[i].initialized = True
+                else:
+                    p._mean_f = out_f
+                p._mean_valid = True
                 p._commit_scratch()
         return True
 

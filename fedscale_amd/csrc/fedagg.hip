@@ -793,6 +793,46 @@ extern "C" int fa_yogi_step(const float* cur, const float* last, float* m, float
   return check_launch("fa_yogi_step");
 }
 
+// fa_yogi_step over every part of a model sharded across this process's GPUs, in one call (round 4: with
+// fa_reduce_parts, config 4's in-process N-GPU finish without a per-part host call chain).  All parts are checked
+// before any launches.
+extern "C" int fa_yogi_step_parts(int32_t n, const float* const* cur, const float* const* last, float* const* m,
+                                  float* const* v, float* const* out, const int64_t* P, float eta, float tau,
+                                  float beta, float omb, float omb2, int32_t flags, fa_stream_t const* streams) {
+  if (n < 1 || !cur || !last || !m || !v || !out || !P || !streams)
+    return fail(FA_E_ARG, "fa_yogi_step_parts: NULL table or n < 1");
+  char what[48], nm[24];
+  for (int i = 0; i < n; ++i) {
+    snprintf(what, sizeof(what), "fa_yogi_step_parts[%d]", i);
+    if (P[i] < 0) return fail(FA_E_ARG, "%s: negative P", what);
+    if (P[i] == 0) continue;
+    if (!cur[i] || !last[i] || !m[i] || !v[i] || !out[i] || !streams[i])
+      return fail(FA_E_ARG, "%s: NULL pointer or stream", what);
+    if (!aligned16(cur[i]) || !aligned16(last[i]) || !aligned16(m[i]) || !aligned16(v[i]) || !aligned16(out[i]))
+      return fail(FA_E_ARG, "%s: pointers must be 16-byte aligned", what);
+    FA_DEVICE_SCOPE(what, streams[i], out[i]);
+    const uint64_t b = cols_bytes(P[i]);
+    const void* ops[5] = {cur[i], last[i], m[i], v[i], out[i]};
+    const char* names[5] = {"cur", "last", "m", "v", "out"};
+    for (int j = 0; j < 5; ++j) {
+      snprintf(nm, sizeof(nm), "%s[%d]", names[j], i);
+      FA_OPERAND(nm, ops[j], b);
+    }
+  }
+  for (int i = 0; i < n; ++i) {
+    if (P[i] == 0) continue;
+    snprintf(what, sizeof(what), "fa_yogi_step_parts[%d]", i);
+    FA_DEVICE_SCOPE(what, streams[i], out[i]);
+    const int64_t P4 = (P[i] + 3) / 4;
+    hipLaunchKernelGGL(k_yogi_step, dim3(stride_grid(P4)), dim3(256), 0, (hipStream_t)streams[i], (const f4*)cur[i],
+                       (const f4*)last[i], (f4*)m[i], (f4*)v[i], (f4*)out[i], P4, eta, tau, beta, omb, omb2,
+                       (flags & FA_YOGI_INIT) ? 1 : 0);
+    const int e = check_launch(what);
+    if (e) return e;
+  }
+  return FA_OK;
+}
+
 // ------------------------------------------------------------------------------------------------
 // q-FedAvg phase 1: delta chain + per-client sum of squares
 // ------------------------------------------------------------------------------------------------

@@ -105,6 +105,24 @@ def reduce_parts(xs, Ks, Ps, outs, acc_ins, streams, *, denom: float, finalize: 
          o_t.ctypes.data, float(denom), fl.ctypes.data, st)
 
 
+def yogi_step_parts(curs, lasts, ms, vs, outs, Ps, streams, *, eta, tau, beta, omb, omb2, init):
+    """fa_yogi_step over every part of a sharded model in one native call (part i on streams[i])."""
+    import ctypes
+
+    import numpy as np
+
+    n = len(curs)
+    for i in range(n):
+        for nm, ts in (("cur", curs), ("last", lasts), ("m", ms), ("v", vs), ("out", outs)):
+            _dev(ts[i], torch.float32, f"{nm}[{i}]", _cols(Ps[i]))
+    tab = lambda ts: np.asarray([t.data_ptr() for t in ts], dtype=np.uint64)  # noqa: E731
+    c_t, l_t, m_t, v_t, o_t = tab(curs), tab(lasts), tab(ms), tab(vs), tab(outs)
+    P = np.asarray(Ps, dtype=np.int64)
+    st = (ctypes.c_void_p * n)(*streams)
+    call("fa_yogi_step_parts", n, c_t.ctypes.data, l_t.ctypes.data, m_t.ctypes.data, v_t.ctypes.data, o_t.ctypes.data,
+         P.ctypes.data, float(eta), float(tau), float(beta), float(omb), float(omb2), FA_YOGI_INIT if init else 0, st)
+
+
 def reduce_mirror(x: torch.Tensor, K: int, P: int, out: torch.Tensor, mirror: torch.Tensor, *,
                   a: Optional[torch.Tensor] = None, acc_in: Optional[torch.Tensor] = None,
                   denom: float = 1.0) -> torch.Tensor:

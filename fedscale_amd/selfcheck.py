@@ -137,7 +137,7 @@ def run(devices, K=24, capacity=7, rounds=2) -> dict:
             handles = {ds.handle: ds for ds in sharded.group.streams}
             bad = 0
             for fn, st, cur in calls:
-                if (fn.startswith("fa_rccl_") and fn not in ("fa_rccl_init", "fa_rccl_destroy")) or fn == "fa_reduce_parts":
+                if (fn.startswith("fa_rccl_") and fn not in ("fa_rccl_init", "fa_rccl_destroy")) or fn in ("fa_reduce_parts", "fa_yogi_step_parts"):
                     bad += int(list(st) != sharded.group.stream_handles())  # a per-part stream table
                 elif fn in ("fa_host_gather", "fa_rccl_init", "fa_rccl_destroy", "fa_host_register",
                             "fa_host_unregister", "fa_h2d_pieces"):

@@ -129,6 +129,14 @@ int fa_reduce_yogi(const float* x, int64_t ld, int32_t K, int64_t P, const float
 int fa_yogi_step(const float* cur, const float* last, float* m, float* v, float* out, int64_t P, float eta,
                  float tau, float beta, float omb, float omb2, int32_t flags, fa_stream_t stream);
 
+/* fa_yogi_step over every part of a model sharded across the GPUs of ONE process, in one call: part i steps cur[i],
+ * last[i], m[i], v[i] -> out[i] (P[i] columns) on streams[i] (never NULL), the same scalars and flags for every part.
+ * Every part is checked before any launches.  With fa_reduce_parts, config 4's in-process finish (optimizers.py:43-63,
+ * yogi.py:15-36 over the model's shards). */
+int fa_yogi_step_parts(int32_t n, const float* const* cur, const float* const* last, float* const* m, float* const* v,
+                       float* const* out, const int64_t* P, float eta, float tau, float beta, float omb, float omb2,
+                       int32_t flags, fa_stream_t const* streams);
+
 /*
  * Number of k_qfed_accum launches one fa_qfed_accumulate call makes for rows of ld floats and P columns,
  * with (chain != 0) or without the fused FedAvg chain: long rows run as column windows of one round of tiles

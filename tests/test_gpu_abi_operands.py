@@ -114,6 +114,9 @@ def _cases(dev, st):
              lambda p: (2, t(p["x"]), host(np.int64, [LD, LD]), host(np.int32, [K, K]), host(np.int64, [P, P]),
                         t(p["acc_in"]), t(p["out"]), ctypes.c_float(4.0), host(np.int32, [FIN | ACC] * 2),
                         t([st, st]))),
+        Case("fa_yogi_step_parts", {k: [f(LD), f(LD)] for k in ("cur", "last", "m", "v", "out")}, ["m", "v", "out"],
+             lambda p: (2, t(p["cur"]), t(p["last"]), t(p["m"]), t(p["v"]), t(p["out"]), host(np.int64, [P, P]), *hp,
+                        0, t([st, st]))),
         # client-side pointer tables (include/fedclient.h)
         Case("fa_prox_update", {"param": tab(1.0), "global": tab(2.0)}, ["param"],
              lambda p: (t(p["param"]), t(p["global"]), numel.ctypes.data, 2, ctypes.c_float(0.1), st)),

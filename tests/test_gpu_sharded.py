@@ -119,9 +119,10 @@ def test_sharded_equals_single_gpu(gpu_device, name):
 LAUNCHES = {"fa_reduce", "fa_reduce_mirror", "fa_reduce_yogi", "fa_yogi_step", "fa_qfed_accumulate", "fa_qfed_hs", "fa_qfed_finalize",
             "fa_sum_rows_f64", "fa_side_accumulate", "fa_side_close", "fa_side_yogi", "fa_side_qfed_accumulate",
             "fa_side_qfed_finalize", "fa_fill_synthetic", "fa_prefix_box_combine", "fa_rccl_all_gather",
-            "fa_rccl_all_reduce", "fa_rccl_gather", "fa_rccl_broadcast", "fa_reduce_parts"}
+            "fa_rccl_all_reduce", "fa_rccl_gather", "fa_rccl_broadcast", "fa_reduce_parts", "fa_yogi_step_parts"}
 #: ... of them, those that take a per-part stream table (one stream per position of the adapter's group)
-TABLE_LAUNCHES = {"fa_rccl_all_gather", "fa_rccl_all_reduce", "fa_rccl_gather", "fa_rccl_broadcast", "fa_reduce_parts"}
+TABLE_LAUNCHES = {"fa_rccl_all_gather", "fa_rccl_all_reduce", "fa_rccl_gather", "fa_rccl_broadcast", "fa_reduce_parts",
+                  "fa_yogi_step_parts"}
 
 
 def _spy_native(monkeypatch):
@@ -188,7 +189,7 @@ def test_every_native_call_runs_on_its_parts_stream(gpu_device, monkeypatch, nam
         list(agg.model_weights)  # the FedAvg mean's D2H runs on the parts' streams too
     launches = _check_part_streams(calls, adapter, f"{name} {sharding}")
     used = {c[1] for c in launches if c[0] not in TABLE_LAUNCHES}
-    used |= {h for c in launches if c[0] == "fa_reduce_parts" for h in c[1]}
+    used |= {h for c in launches if c[0] in ("fa_reduce_parts", "fa_yogi_step_parts") for h in c[1]}
     assert used == set(adapter.group.stream_handles()), "every part launched on its own stream"
     if sc.meta["policy"] == "q-fedavg":
         assert any(c[0] in ("fa_rccl_all_gather", "fa_sum_rows_f64") for c in launches)
@@ -616,17 +617,48 @@ def test_inproc_bench_module_rehearsal(gpu_device):
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-m", "fedscale_amd.inproc_bench", "--devices", "0,0", "--clients", "16",
-                        "--params", "1000000", "--rounds", "3"], cwd=root, capture_output=True, text=True,
-                       timeout=300)
+                        "--params", "1000000", "--rounds", "3", "--policies", "fedavg,fed-yogi"], cwd=root,
+                       capture_output=True, text=True, timeout=300)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert lines, (r.returncode, r.stderr[-2000:])
-    rep = json.loads(lines[-1])
-    assert r.returncode == 0 and rep["ok"], rep
-    assert rep["transport"] == "copy" and rep["distinct_gpus"] is False
-    assert len(rep["part_kernel_ms"]) == 2 and all(t > 0 for t in rep["part_kernel_ms"])
-    for k in ("inproc_round_ms", "egress_ms", "inproc_round_ms_incl_egress", "speedup_vs_one_gpu"):
-        assert rep[k] > 0, k
-    assert rep["one_gpu"]["round_ms"] > 0
+    both = json.loads(lines[-1])
+    assert r.returncode == 0 and both["ok"], both
+    for pol in ("fedavg", "fed-yogi"):
+        rep = both["policies"][pol]
+        assert rep["transport"] == "copy" and rep["distinct_gpus"] is False
+        assert len(rep["part_kernel_ms"]) == 2 and all(t > 0 for t in rep["part_kernel_ms"])
+        for k in ("inproc_round_ms", "egress_ms", "inproc_round_ms_incl_egress", "speedup_vs_one_gpu"):
+            assert rep[k] > 0, (pol, k)
+        assert rep["one_gpu"]["round_ms"] > 0
+
+
+def test_batched_yogi_finish_matches_per_part(gpu_device):
+    """Config 4's in-process finish: fa_reduce_parts + fa_yogi_step_parts (one native call per pass over every
+    part) gives the same bits as each part's own two-pass finish, over three rounds (the YoGi state carries)."""
+    from fedscale_amd import synth
+    from fedscale_amd.cloud.internal.sharded_model_adapter import ShardedModelAdapter
+    from fedscale_amd.inproc_bench import _model, _optimizer
+
+    K, P = 24, 300_000
+    outs = []
+    for batched in (True, False):
+        ad = ShardedModelAdapter(_model(P, 5), optimizer=_optimizer("fed-yogi", 0), devices=[0, 0, 0],
+                                 staging_capacity=K)
+        ad.FINISH_PARTS_AT_ONCE = batched
+        got = []
+        for rr in range(3):
+            rnd = ad.begin_round(K, "fedavg", capacity=K)
+            for i, (p, r) in enumerate(zip(ad.parts, rnd.rounds)):
+                with p.dstream:
+                    synth.fill(r.staging.x, K, p.layout.P, seed=100 * rr + i)
+            rnd.adopt_resident(K)
+            ad.apply_round(rnd, float(np.float32(K)), float(K))
+            got.append([w.clone() for w in ad.get_weights()])
+        outs.append(got)
+        ad.close()
+    for rr, (a, b) in enumerate(zip(*outs)):
+        for i, (x, y) in enumerate(zip(a, b)):
+            assert torch.equal(x, y), f"round {rr} tensor {i}"
 
 
 @pytest.mark.parametrize("parts", [2, 3])
