@@ -20,6 +20,22 @@ def _u64(ptrs):
     return np.asarray(ptrs, dtype=np.uint64)
 
 
+_STREAMS = []
+
+
+def _stream():
+    """A non-null stream (the per-part tables, fa_reduce_parts / fa_yogi_step_parts, refuse the null stream),
+    created blocking (hipStreamCreate's default flags), so it is ordered after the tensors torch fills on the null
+    stream; the tests synchronize the whole device."""
+    if not _STREAMS:
+        hip = ctypes.CDLL("libamdhip64.so")
+        hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        s = ctypes.c_void_p()
+        assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+        _STREAMS.append(s.value)
+    return _STREAMS[0]
+
+
 class Case:
     """An entry point, its operands (device tensors, or lists of them for pointer tables), the operands a
     launch writes, and how the ABI arguments are formed from a {name: pointer or [pointers]} map."""
@@ -176,7 +192,7 @@ def test_pageable_operand_in_every_position_is_rejected_before_any_launch(gpu_de
     from fedscale_amd import _native as N
 
     lib = N.load()
-    st = torch.cuda.current_stream().cuda_stream
+    st = _stream()
     pageable = np.zeros(1 << 20, dtype=np.float64)  # plain malloc'd host memory: pageable
     bad = pageable.ctypes.data
     cases, keep = _cases(gpu_device, st)
@@ -212,7 +228,7 @@ def test_pinned_host_operand_only_where_the_header_allows_it(gpu_device):
     from fedscale_amd import _native as N
 
     lib = N.load()
-    st = torch.cuda.current_stream().cuda_stream
+    st = _stream()
     pinned = torch.zeros(1 << 17, dtype=torch.float64).pin_memory()
     cases, keep = _cases(gpu_device, st)
     for case in cases:
@@ -242,7 +258,7 @@ def test_operand_extent_beyond_its_allocation_is_rejected(gpu_device):
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t]
     hip.hipFree.argtypes = [ctypes.c_void_p]
-    st = torch.cuda.current_stream().cuda_stream
+    st = _stream()
     big = 1 << 22
     cur = torch.ones(big, device=gpu_device)
     m, v, out = (torch.zeros(big, device=gpu_device) for _ in range(3))
@@ -275,7 +291,7 @@ def test_rccl_buffers_are_checked(gpu_device):
     devs = np.zeros(1, dtype=np.int32)
     N.call("fa_rccl_init", 1, devs.ctypes.data, ctypes.byref(comm))
     try:
-        st = torch.cuda.current_stream().cuda_stream
+        st = _stream()
         send = torch.ones(64, device=gpu_device)
         recv = torch.zeros(64, device=gpu_device)
         pageable = np.zeros(64, dtype=np.float32)
@@ -304,7 +320,7 @@ def test_h2d_pieces_checks_every_piece(gpu_device):
     from fedscale_amd import _native as N
 
     lib = N.load()
-    st = torch.cuda.current_stream().cuda_stream
+    st = _stream()
     host = np.arange(1 << 18, dtype=np.float32)  # pageable until registered
     pinned = torch.arange(1 << 10, dtype=torch.float32).pin_memory()
     dst = torch.zeros(1 << 18, device=gpu_device)
