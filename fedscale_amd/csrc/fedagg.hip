@@ -868,8 +868,12 @@ static inline int qf_grid(bool chain) { return chain ? QF_CHAIN_GRID : QF_GRID; 
 #ifndef QF_BALANCE
 #define QF_BALANCE 1  // 0: always full-width tiles (plain grid-stride)
 #endif
+// Clients per fa_qfed_accumulate call (a DeviceRound chunk).  LDS: 4 waves x QF_MAXK clients x 8 B per workgroup
+// (64 KiB at 2048).  Round 4: 2048 halves the passes (and launch boundaries) of a 10,000-client round; config 5's
+// shard of 8 (10,000 x 12.5 M) 70.9 ms every run against 71.0-74.1 ms at 1024, interleaved whole-library A/B on
+// one box (tools/ab_c5.sh, profiles/r04_ab_c5_maxk.log).
 #ifndef QF_MAXK
-#define QF_MAXK 1024  // LDS: 4 waves x 1024 clients x 8 B = 32 KiB per workgroup
+#define QF_MAXK 2048
 #endif
 static_assert(QF_MAXK % 4 == 0 && QF_MAXK <= 4096, "QF_MAXK: a multiple of 4, <= 4096 (LDS)");
 

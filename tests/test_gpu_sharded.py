@@ -488,7 +488,8 @@ def test_nccl_process_group_collectives_world1(gpu_device):
         dist.destroy_process_group()
 
 
-def test_egress_never_mixes_part_versions(gpu_device):
+@pytest.mark.parametrize("at_once", [True, False], ids=["parts_at_once", "per_part"])
+def test_egress_never_mixes_part_versions(gpu_device, at_once):
     """A servicer thread asking for the model while the main thread is between two parts' commits gets
     the previous version whole (aggregator.py:177-178: 20 servicer threads read the model while the main
     loop applies rounds): part 0 already holds the new model, part 1 the old one, the version is still
@@ -521,10 +522,11 @@ def test_egress_never_mixes_part_versions(gpu_device):
             agg1.on_result(res)
         want.append([t.numpy().copy() for t in single.get_weights()])
 
+    sharded.FINISH_PARTS_AT_ONCE = at_once
     started, done, seen = threading.Event(), threading.Event(), {}
-    orig = sharded.parts[1].apply_round
+    orig = sharded.parts[1]._commit_scratch
 
-    def slow_apply(*a, **k):  # part 0 has committed round 2; part 1 has not
+    def slow_commit(*a, **k):  # part 0 has committed round 2; part 1 has not
         started.set()
         assert done.wait(60), "servicer thread did not finish"
         return orig(*a, **k)
@@ -540,7 +542,7 @@ def test_egress_never_mixes_part_versions(gpu_device):
     agg.start_round(len(rounds[0]))
     for res in rounds[0]:  # round 1, never read back before the race
         agg.on_result(res)
-    sharded.parts[1].apply_round = slow_apply
+    sharded.parts[1]._commit_scratch = slow_commit
     th = threading.Thread(target=servicer)
     th.start()
     agg.start_round(len(rounds[1]))
