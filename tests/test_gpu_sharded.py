@@ -699,7 +699,11 @@ def test_registered_payload_ingress_is_bit_exact(gpu_device, parts):
             else:
                 res = {"client_id": k, "update_weight": up, "moving_loss": 1.0}
             agg.on_result(res)
-        assert_state_equal(sharded.get_weights(), fedavg_close(acc, K), f"round {r}")
+        want = fedavg_close(acc, K)  # the reference's model_weights (int64 entries as float64 means)
+        assert_state_equal(list(agg.model_weights), want, f"round {r} mean")
+        # ... loaded into the model (load_state_dict's copy_: float64 -> int64 truncates)
+        loaded = [torch.as_tensor(np.asarray(w)).to(d).numpy() for w, d in zip(want, dtypes)]
+        assert_state_equal(sharded.get_weights(), loaded, f"round {r} model")
     assert sharded.registered_uploads == 2 * sum(1 for k in range(K) if k % 3 != 2)
     sharded.close()
     assert not sharded._regs
