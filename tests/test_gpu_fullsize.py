@@ -210,7 +210,7 @@ def test_c5_qfedavg_shard_k10000_chain_deferred_as_the_drop_in_runs_it(gpu_devic
     sqh = sq.cpu().numpy()
     allc = np.arange(P)
     Lfull = last[:P].cpu().numpy()
-    for k in (0, chunk - 1, chunk, 5 * chunk + 17, K - 1):  # chunk seams included
+    for k in (0, chunk - 1, chunk, (nch - 1) * chunk + 17, K - 1):  # chunk seams included
         g = (Lfull - synth.host_columns(seed, [k], allc)[0]) / np.float32(lr)
         ref = np.sum((g * g).astype(np.float64))
         assert abs(sqh[k] - ref) <= 1e-9 * ref
