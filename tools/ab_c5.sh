@@ -1,14 +1,14 @@
 #!/bin/bash
 # Interleaved A/B of whole libraries on config 5's shard of 8 as bench.py times it (10,000 x 12.5 M q-FedAvg, chain
 # launches, deferred gathers): FEDAGG_LIB=fedscale_amd/ab/libfedagg_<name>.so, alternating, 3 runs each.
-#   bash tools/ab_c5.sh base maxk2048
+#   bash tools/ab_c5.sh base maxk2048        (AB_PARAMS=100000000 AB_STEPS=2: the one-GPU config 5)
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 cd $ROOT
 mkdir -p $ROOT/gpurun_out
 for rep in 1 2 3; do
   for name in "$@"; do
-    out=$(FEDAGG_LIB=$ROOT/fedscale_amd/ab/libfedagg_$name.so timeout -k 10 240 python bench.py --config c5 --params 12500000 --steps 3 --warmup 1 --cpu-seconds 0 --no-other-configs 2>$ROOT/gpurun_out/ab_${name}_err.log | grep '^{') || { echo "$name failed"; tail -5 $ROOT/gpurun_out/ab_${name}_err.log; exit 1; }
+    out=$(FEDAGG_LIB=$ROOT/fedscale_amd/ab/libfedagg_$name.so timeout -k 10 240 python bench.py --config c5 --params ${AB_PARAMS:-12500000} --steps ${AB_STEPS:-3} --warmup 1 --cpu-seconds 0 --no-other-configs 2>$ROOT/gpurun_out/ab_${name}_err.log | grep '^{') || { echo "$name failed"; tail -5 $ROOT/gpurun_out/ab_${name}_err.log; exit 1; }
     python -c "import json,sys; d=json.loads(sys.argv[1]); print('$name', 'rep $rep', 'round_ms %.3f' % d['ms_per_step'], 'kernel_ms %.3f' % d['kernel_ms'], 'GB/s %.1f' % d['hbm_gbps'], 'passes', d['config'].get('streamed_passes'))" "$out"
   done
 done
