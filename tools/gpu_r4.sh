@@ -9,6 +9,7 @@
 #   c4       config 4 as the drop-in runs it (mean, then k_yogi_step): kernel trace + stats
 #   c5       config 5's shard of 8: kernel trace + stats, FETCH_SIZE / WRITE_SIZE (MI355X_MICROARCH.md recipe)
 #   head     headline kernel trace + stats
+#   c4pmc / headpmc  FETCH_SIZE / WRITE_SIZE passes of config 4's unfused round / the headline
 #   rehearse 2- and 4-rank gloo rehearsals of bench.py --gpus N on the one card (plumbing of the N-GPU fields)
 set -o pipefail
 ROOT=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -55,6 +56,13 @@ c5)
   for c in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $OUT/${T}_c5_$c -o run -- python3 bench.py $ARGS > $OUT/${T}_c5_$c.log 2>&1 || { tail -5 $OUT/${T}_c5_$c.log; exit 1; }
   done ;;
+c4pmc|headpmc)
+  # FETCH_SIZE / WRITE_SIZE of config 4's unfused round (k_reduce x 4 + k_yogi_step) or the headline, one pass each
+  [ $STAGE = c4pmc ] && ARGS="--config c4 --steps 3 --warmup 1 --cpu-seconds 0 --no-other-configs" || ARGS="--steps 3 --warmup 1 --cpu-seconds 0 --no-other-configs"
+  for c in FETCH_SIZE WRITE_SIZE; do
+    timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $OUT/${T}_${STAGE}_$c -o run -- python3 bench.py $ARGS > $OUT/${T}_${STAGE}_$c.log 2>&1 || { tail -5 $OUT/${T}_${STAGE}_$c.log; exit 1; }
+  done
+  grep '^{' $OUT/${T}_${STAGE}_FETCH_SIZE.log | cut -c1-300 ;;
 head)
   ARGS="--steps 12 --warmup 3 --cpu-seconds 0 --no-other-configs"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/${T}_head_prof -o run -- python3 bench.py $ARGS > $OUT/${T}_head_prof.log 2>&1 || { tail -20 $OUT/${T}_head_prof.log; exit 1; }

@@ -2,7 +2,7 @@
 
 gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reports exactly half of the bytes of a wide
 coalesced streaming read (16 B/lane dwordx4) -> x2; WRITE_SIZE is exact for 16 B/lane stores.  Both
-counters are in KiB.  usage: python tools/pmc_parse.py <fetch_dir> <write_dir> <workload_key> <alg_bytes>
+counters are in KiB.  usage: python tools/pmc_parse.py <fetch_dir> <write_dir> <workload_key> <alg_bytes> [kernel | "k1*n1+k2*n2"] [launches]
 """
 import csv
 import glob
@@ -30,11 +30,20 @@ def main():
     kern = sys.argv[5] if len(sys.argv) > 5 else "k_reduce"
     launches = int(sys.argv[6]) if len(sys.argv) > 6 else 1
     alg = alg / launches
-    f = per_dispatch(fetch_dir, "FETCH_SIZE", kern)
-    w = per_dispatch(write_dir, "WRITE_SIZE", kern)
-    if not f or not w:
-        raise SystemExit(f"no {kern} dispatches found (fetch {len(f)}, write {len(w)})")
-    fkb, wkb = sum(f) / len(f), sum(w) / len(w)
+    # kern "a*4+b*1": a step of several kernels (4 launches of a, 1 of b); per launch = the step's bytes / launches
+    terms = [(t.split("*")[0], int(t.split("*")[1]) if "*" in t else 1) for t in kern.split("+")]
+    fkb = wkb = 0.0
+    ndisp = 0
+    for name, count in terms:
+        f = per_dispatch(fetch_dir, "FETCH_SIZE", name)
+        w = per_dispatch(write_dir, "WRITE_SIZE", name)
+        if not f or not w:
+            raise SystemExit(f"no {name} dispatches found (fetch {len(f)}, write {len(w)})")
+        scale = count / launches if len(terms) > 1 else 1.0
+        fkb += scale * sum(f) / len(f)
+        wkb += scale * sum(w) / len(w)
+        ndisp += len(f)
+    f = [None] * ndisp
     hbm = (2 * fkb + wkb) * 1024
     out_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     db = json.load(open(out_path)) if os.path.exists(out_path) else {}
