@@ -75,6 +75,8 @@ def parse():
                          "collective, bit-exact); clients: each rank reduces its own K clients over the whole "
                          "model, then one RCCL all-reduce of the partial sums (state.py)")
     ap.add_argument("--no-reassemble", action="store_true", help="skip the egress all-gather timing at N>1")
+    ap.add_argument("--rest", type=float, default=None,
+                    help="seconds the card idles before each heavy timed region (default %g; 0 = off)" % REST_S)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the headline CPU sample (0 = skip "
                                                                      "every CPU leg)")
     ap.add_argument("--seed", type=int, default=2024)
@@ -585,12 +587,31 @@ def _all_ranks(val: float, dev, world, backend) -> list:
     return [float(o.cpu()[0]) for o in out]
 
 
+#: seconds the card idles before each heavy timed region (--rest).  A FedScale aggregator's GPU works in bursts: one
+#: reduction per round, idle while the clients train.  After minutes of back-to-back streaming the same launches run
+#: 3-4 % slower (the card's power/thermal state, not the allocation history: tools/inline_probe.py,
+#: profiles/r04_inline_probe.log), so without a rest every config of the line would be timed in whatever state the
+#: configs before it left the card.  Outside the timed region; 0 turns it off.
+REST_S = 12.0
+
+
+def _rest(w, steps, dev):
+    import torch
+
+    if REST_S > 0 and w.alg_bytes * max(1, steps) > 20e9:  # heavy regions only (c2's 0.4 GB rounds need none)
+        torch.cuda.synchronize(dev)
+        time.sleep(REST_S)
+        return REST_S
+    return 0.0
+
+
 def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend):
     """Warmup, then exactly ``steps`` rounds between barrier + synchronize; (wall s, mean dominant-kernel
-    ms), both max over ranks."""
+    ms), both max over ranks.  Heavy regions start from a rested card (``REST_S``; every rank rests alike)."""
     import numpy as np
     import torch
 
+    w.rest_s = _rest(w, steps, dev)
     for _ in range(warmup):
         w.step()
     split = w.yogi is not None and not w.cmode  # FedYoGi: a third event between the mean and the YoGi step
@@ -622,7 +643,7 @@ def config_line(name, cfg, dev, rank, world, shards, seed, backend, steps=5, war
            "params_per_gpu": w.P, "resident_clients": w.C, "passes": len(w.passes), "round_ms": ms,
            "client_updates_per_s": cfg["clients"] / (ms * 1e-3),
            "hbm_gbps_per_gpu": w.alg_bytes / (ms * 1e-3) / 1e9, "dominant_kernel_ms": kern_max,
-           "hbm_gbps_kernel": w.alg_bytes / (kern_max * 1e-3) / 1e9}
+           "hbm_gbps_kernel": w.alg_bytes / (kern_max * 1e-3) / 1e9, "card_rest_s": w.rest_s}
     if getattr(w, "split_ms", None):
         from fedscale_amd import kernels as kx
 
@@ -770,6 +791,7 @@ def one_gpu_reference(policy, K, P, dev, seed, steps=5, warmup=2) -> dict:
     from fedscale_amd.state import ShardGroup
 
     w = Workload(policy, K, P, 0, 1, dev, seed, ShardGroup(0, 1), budget_fraction=MEM_FRACTION)
+    _rest(w, steps, dev)  # from the same card state as the N-rank region it is compared with
     for _ in range(warmup):
         w.step()
     import torch
@@ -785,7 +807,10 @@ def one_gpu_reference(policy, K, P, dev, seed, steps=5, warmup=2) -> dict:
 
 
 def main():
+    global REST_S
     args = parse()
+    if args.rest is not None:
+        REST_S = max(0.0, args.rest)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -920,6 +945,7 @@ def main():
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic full-weight client updates (base + noise, hash-generated on device), HBM-resident",
             "host_numa_node": numa_node,
+            "card_rest_s": REST_S,
             "config": config,
             "hbm_gbps": achieved,
             "kernel_ms": kern_ms_max,
