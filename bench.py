@@ -439,6 +439,7 @@ class Workload:
             synth.fill(x, self.C, self.P, seed=seed + 7919 * rank + 31 * i)
             self.xs.append(x)
         self.it = 0
+        self.rest_s = 0.0  # the card's idle before this workload's timed region (time_workload)
         self.out = torch.zeros(ld, dtype=torch.float32, device=dev)
         self.acc = torch.zeros(ld, dtype=torch.float32, device=dev) if (self.cmode or len(self.passes) > 1) else None
         self.Kg = K * world if self.cmode else K  # clients in the round (client mode: every rank brings K)
