@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, "libfedagg.so"))
-ABI_VERSION = 3  # fedagg.hip FA_ABI_VERSION
+ABI_VERSION = 4  # fedagg.hip FA_ABI_VERSION
 
 FA_ACCUMULATE = 1
 FA_FINALIZE = 2
@@ -33,6 +33,8 @@ _c_void_p, _i32, _i64, _f32, _f64, _u32 = (ctypes.c_void_p, ctypes.c_int32, ctyp
 # name -> (restype, argtypes);  must list every symbol of include/fedagg.h and include/fedclient.h
 SIGNATURES = {
     "fa_abi_version": (_i32, []),
+    "fa_build_id": (ctypes.c_char_p, []),
+    "fa_build_defs": (ctypes.c_char_p, []),
     "fa_last_error_string": (ctypes.c_char_p, []),
     "fa_pointer_kind": (_i32, [_c_void_p]),
     "fa_reduce": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _f32, _i32, _c_void_p]),
@@ -79,6 +81,9 @@ SIGNATURES = {
     "fa_rccl_all_reduce": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i64, _i32, _c_void_p]),
     "fa_rccl_gather": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i64, _i32, _i32, _c_void_p]),
     "fa_rccl_broadcast": (_i32, [_c_void_p, _c_void_p, _i64, _i32, _i32, _c_void_p]),
+    "fa_rccl_comm_info": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "fa_rccl_unique_id": (_i32, [_c_void_p]),
+    "fa_rccl_init_rank": (_i32, [_i32, _c_void_p, _i32, _i32, ctypes.POINTER(_c_void_p)]),
     # include/fedclient.h (client-side handlers; pointer tables are host arrays)
     "fa_prox_update": (_i32, [_c_void_p, _c_void_p, _c_void_p, _i32, _f32, _c_void_p]),
     "fa_sgd_prox_step": (_i32, [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _i32, _f32, _f32, _f64,
@@ -96,28 +101,61 @@ SIGNATURES = {
 }
 
 _lib = None
+_info = None
 _lock = threading.Lock()
 
 
-def load(path: str = LIB_PATH):
-    """Load (once) and type the shared library.  Raises FedAggError when it is absent."""
-    global _lib
+def check_build(lib, path: str, tree: str = None) -> dict:
+    """The library's build id against the one the sources of ``tree`` (default: this checkout) produce with the
+    library's own extra definitions (fedscale_amd/buildinfo.py); FedAggError on a mismatch — a library built
+    from other sources (a stale or foreign binary) is never used."""
+    from . import buildinfo
+
+    bid = lib.fa_build_id().decode(errors="replace")
+    defs = lib.fa_build_defs().decode(errors="replace")
+    tree = tree or buildinfo.ROOT
+    try:
+        want = buildinfo.source_id(defs, root=tree)
+    except OSError as e:
+        raise FedAggError(f"{path}: cannot verify its build id {bid}: the library's sources are not readable "
+                          f"under {tree} ({e})")
+    if bid != want:
+        raise FedAggError(f"{path}: build id {bid} (defs {defs!r}), but the sources under {tree} build {want}: the "
+                          f"library is stale or was built from other sources (run `python __graft_entry__.py`)")
+    return {"path": os.path.abspath(path), "build_id": bid, "defs": defs, "verified_against": tree}
+
+
+def load(path: str = None, tree: str = None):
+    """Load (once) and type the shared library.  Raises FedAggError when it is absent, has another ABI version,
+    or was not built from the sources in the tree (``check_build``)."""
+    global _lib, _info
     with _lock:
-        if _lib is not None:
+        if _lib is not None and path is None and tree is None:
             return _lib
+        path = path or LIB_PATH
         if not os.path.exists(path):
             raise FedAggError(f"{path} not found: the HIP extension is not built "
                               f"(run `python __graft_entry__.py` to build it; there is no CPU fallback)")
         lib = ctypes.CDLL(path)
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                raise FedAggError(f"{path}: no symbol {name} (an older build; run `python __graft_entry__.py`)")
             fn.restype = res
             fn.argtypes = args
         v = lib.fa_abi_version()
         if v != ABI_VERSION:
             raise FedAggError(f"{path}: ABI version {v}, expected {ABI_VERSION}")
-        _lib = lib
+        info = check_build(lib, path, tree)
+        if tree is None:
+            _lib, _info = lib, info
         return lib
+
+
+def build_info() -> dict:
+    """{path, build_id, defs, verified_against} of the loaded library (loads it)."""
+    load()
+    return dict(_info)
 
 
 def call(name: str, *args):

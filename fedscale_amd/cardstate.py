@@ -1,0 +1,149 @@
+"""The card's state while a timed region runs: board power, edge / junction / HBM temperatures and the memory and
+shader clock levels, sampled from the amdgpu driver's sysfs files of THIS process's GPU (read-only; no SMI process,
+no privileges).  bench.py records a summary per heavy region, so a rested-card figure and a sustained one carry the
+signal that separates them.
+
+    with CardSampler(dev) as s:
+        ... timed region ...
+    s.summary()  # {"samples": n, "power_w": {...}, "temp_junction_c": {...}, "mclk_mhz": {...}, ...}
+
+Sources (amdgpu hwmon ABI): ``hwmon*/power1_average`` or ``power1_input`` (µW), ``temp*_input`` (m°C) named by
+``temp*_label`` (edge, junction, mem), ``pp_dpm_mclk`` / ``pp_dpm_sclk`` (the level marked ``*``).  A file the
+box does not expose is left out of the summary (``missing`` lists it); nothing here raises.
+"""
+from __future__ import annotations
+
+import glob
+import os
+import re
+import threading
+import time
+
+
+def _pci_dir(dev) -> str | None:
+    """/sys/bus/pci/devices/<domain:bus:dev.fn> of a torch CUDA device (HIP_VISIBLE_DEVICES-aware: torch reports
+    the PCI address of the device it sees)."""
+    try:
+        import torch
+
+        p = torch.cuda.get_device_properties(dev)
+        dom, bus, d = getattr(p, "pci_domain_id", 0), getattr(p, "pci_bus_id", None), getattr(p, "pci_device_id", None)
+        if bus is None or d is None:
+            return None
+        path = "/sys/bus/pci/devices/%04x:%02x:%02x.0" % (dom, bus, d)
+        return path if os.path.isdir(path) else None
+    except Exception:
+        return None
+
+
+def _read(path: str):
+    try:
+        with open(path) as f:
+            return f.read()
+    except OSError:
+        return None
+
+
+def _level(text):
+    """MHz of the level pp_dpm_* marks as current ('1: 1300Mhz *')."""
+    if not text:
+        return None
+    for line in text.splitlines():
+        if line.rstrip().endswith("*"):
+            m = re.search(r"(\d+)\s*[Mm][Hh]z", line)
+            if m:
+                return float(m.group(1))
+    return None
+
+
+class CardSampler:
+    """Samples the card every ``period_s`` on a daemon thread between ``start()`` and ``stop()``."""
+
+    def __init__(self, dev, period_s: float = 0.1):
+        self.period = period_s
+        self.pci = _pci_dir(dev)
+        self.files = {}
+        self.missing = []
+        if self.pci:
+            hw = sorted(glob.glob(os.path.join(self.pci, "hwmon", "hwmon*")))
+            if hw:
+                h = hw[0]
+                pw = [os.path.join(h, n) for n in ("power1_average", "power1_input")]
+                pw = [p for p in pw if _read(p) is not None]
+                if pw:
+                    self.files["power_w"] = (pw[0], lambda t: float(t) / 1e6)
+                for tin in sorted(glob.glob(os.path.join(h, "temp*_input"))):
+                    label = (_read(tin.replace("_input", "_label")) or os.path.basename(tin)).strip().lower()
+                    if _read(tin) is not None:
+                        self.files[f"temp_{label}_c"] = (tin, lambda t: float(t) / 1e3)
+            for name in ("pp_dpm_mclk", "pp_dpm_sclk", "pp_dpm_fclk"):
+                p = os.path.join(self.pci, name)
+                if _read(p) is not None:
+                    self.files[name[7:] + "_mhz"] = (p, _level)
+        for want in ("power_w", "temp_junction_c", "temp_mem_c", "mclk_mhz", "sclk_mhz"):
+            if want not in self.files:
+                self.missing.append(want)
+        self.samples = {k: [] for k in self.files}
+        self._stop = threading.Event()
+        self._t = None
+        self.t0 = self.t1 = None
+
+    def sample(self):
+        for k, (path, conv) in self.files.items():
+            t = _read(path)
+            if t is None:
+                continue
+            try:
+                v = conv(t)
+            except ValueError:
+                v = None
+            if v is not None:
+                self.samples[k].append(v)
+
+    def _run(self):
+        while not self._stop.is_set():
+            self.sample()
+            self._stop.wait(self.period)
+
+    def start(self):
+        self.t0 = time.perf_counter()
+        if self.files:
+            self._t = threading.Thread(target=self._run, name="card-sampler", daemon=True)
+            self._t.start()
+        return self
+
+    def stop(self):
+        self._stop.set()
+        if self._t is not None:
+            self._t.join(timeout=2)
+        self.t1 = time.perf_counter()
+        return self
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+        return False
+
+    def summary(self) -> dict:
+        out = {"seconds": round((self.t1 or time.perf_counter()) - (self.t0 or 0), 3), "source": self.pci}
+        n = 0
+        for k, vs in self.samples.items():
+            if not vs:
+                continue
+            n = max(n, len(vs))
+            s = sorted(vs)
+            out[k] = {"mean": round(sum(vs) / len(vs), 2), "min": s[0], "max": s[-1],
+                      "median": s[len(s) // 2], "last": vs[-1]}
+        out["samples"] = n
+        if self.missing:
+            out["missing"] = list(self.missing)
+        return out
+
+
+def snapshot(dev) -> dict:
+    """One reading of every source (the card's state before a region)."""
+    s = CardSampler(dev)
+    s.sample()
+    return {k: v[0] for k, v in s.samples.items() if v} | ({"missing": s.missing} if s.missing else {})

@@ -35,7 +35,18 @@
 // 2: fa_qfed_accumulate gained `chain`, fa_sgd_prox_step's dampening became double, and every launching
 //    entry point resolves its device from the stream / output pointer (fa_device.h)
 // 3: fa_qfed_accumulate takes the workspace's size, fa_qfed_workspace_bytes the call's (ld, P) (deferred gathers)
-#define FA_ABI_VERSION 3
+// 4: fa_build_id / fa_build_defs, fa_rccl_comm_info
+#define FA_ABI_VERSION 4
+
+// The build id (fedscale_amd/buildinfo.py): a hash of the sources, headers and flags this library was compiled
+// from, passed in by the build.  _native.load() recomputes it from the tree and refuses a library that differs.
+#ifndef FA_BUILD_ID
+#define FA_BUILD_ID "unset"  // a build outside buildinfo.py: no loader accepts it
+#endif
+#ifndef FA_BUILD_DEFS
+#define FA_BUILD_DEFS ""
+#endif
+__attribute__((used)) static const char fa_build_marker[] = "FA_BUILD_ID=" FA_BUILD_ID;
 
 // FA_TUNING 1 (tools/build_*variants.sh) compiles the measured-and-rejected alternatives kept for re-measurement:
 // the second q-FedAvg design (k_qfed_accum2), the level cascade of fixed variants, the multi-round capped grid,
@@ -79,6 +90,8 @@ extern "C" __attribute__((visibility("hidden"))) int fa_internal_set_error(int c
 }
 
 extern "C" int fa_abi_version(void) { return FA_ABI_VERSION; }
+extern "C" const char* fa_build_id(void) { return fa_build_marker + sizeof("FA_BUILD_ID=") - 1; }
+extern "C" const char* fa_build_defs(void) { return FA_BUILD_DEFS; }
 extern "C" int fa_pointer_kind(const void* p) { return fa_host_mapped(p); }
 extern "C" const char* fa_last_error_string(void) { return g_err; }
 

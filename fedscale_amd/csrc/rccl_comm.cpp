@@ -13,6 +13,7 @@
 #include <dlfcn.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <string.h>
 
 #include <mutex>
 #include <new>
@@ -37,6 +38,11 @@ struct RcclApi {
   decltype(&ncclBroadcast) broadcast = nullptr;
   decltype(&ncclGetErrorString) error_string = nullptr;
   decltype(&ncclGetVersion) version = nullptr;
+  decltype(&ncclCommCount) count = nullptr;
+  decltype(&ncclCommCuDevice) cu_device = nullptr;
+  decltype(&ncclCommUserRank) user_rank = nullptr;
+  decltype(&ncclGetUniqueId) unique_id = nullptr;
+  decltype(&ncclCommInitRank) init_rank = nullptr;
   bool ok = false;
 };
 
@@ -61,9 +67,15 @@ void load_api() {
   FA_SYM(broadcast, "ncclBroadcast");
   FA_SYM(error_string, "ncclGetErrorString");
   FA_SYM(version, "ncclGetVersion");
+  FA_SYM(count, "ncclCommCount");
+  FA_SYM(cu_device, "ncclCommCuDevice");
+  FA_SYM(user_rank, "ncclCommUserRank");
+  FA_SYM(unique_id, "ncclGetUniqueId");
+  FA_SYM(init_rank, "ncclCommInitRank");
 #undef FA_SYM
   g_api.ok = g_api.init_all && g_api.destroy && g_api.group_start && g_api.group_end && g_api.all_gather &&
-             g_api.all_reduce && g_api.gather && g_api.broadcast && g_api.error_string;
+             g_api.all_reduce && g_api.gather && g_api.broadcast && g_api.error_string && g_api.count &&
+             g_api.cu_device && g_api.user_rank && g_api.unique_id && g_api.init_rank;
 }
 
 const RcclApi* api() {
@@ -72,7 +84,7 @@ const RcclApi* api() {
 }
 
 struct Comm {
-  int n = 0;
+  int n = 0;                       // communicators this handle holds (the devices this process drives)
   std::vector<ncclComm_t> comms;
   std::vector<int> devs;  // device of comms[i]
 };
@@ -190,6 +202,76 @@ extern "C" int fa_rccl_init(int32_t ndev, const int32_t* devs, void** comm_out) 
     return err(FA_E_HIP, "fa_rccl_init: ncclCommInitAll", r);
   }
   *comm_out = c;
+  return FA_OK;
+}
+
+// One rank of a communicator that spans processes (one process per GPU): the bench's SPMD ranks open one over
+// their own GPU to record what RCCL itself sees (fa_rccl_comm_info), next to torch.distributed's view.
+extern "C" int fa_rccl_unique_id(void* id_out) {
+  if (!id_out) return fa_internal_set_error(FA_E_ARG, "fa_rccl_unique_id: NULL");
+  const RcclApi* a = api();
+  if (!a) return fa_internal_set_error(FA_E_HIP, "fa_rccl_unique_id: RCCL could not be loaded");
+  ncclUniqueId id;
+  ncclResult_t r = a->unique_id(&id);
+  if (r != ncclSuccess) return err(FA_E_HIP, "fa_rccl_unique_id: ncclGetUniqueId", r);
+  memcpy(id_out, &id, sizeof(id));
+  return FA_OK;
+}
+
+extern "C" int fa_rccl_init_rank(int32_t nranks, const void* id, int32_t rank, int32_t device, void** comm_out) {
+  if (nranks < 1 || rank < 0 || rank >= nranks || !id || !comm_out || device < 0)
+    return fa_internal_set_error(FA_E_ARG, "fa_rccl_init_rank: bad arguments");
+  const RcclApi* a = api();
+  if (!a) return fa_internal_set_error(FA_E_HIP, "fa_rccl_init_rank: RCCL could not be loaded");
+  int prev = -1;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+    (void)hipGetLastError();
+    return fa_internal_set_error(FA_E_HIP, "fa_rccl_init_rank: cannot select the device");
+  }
+  Comm* c = new (std::nothrow) Comm();
+  if (!c) {
+    (void)hipSetDevice(prev);
+    return fa_internal_set_error(FA_E_HIP, "fa_rccl_init_rank: out of memory");
+  }
+  c->n = 1;
+  c->comms.resize(1);
+  c->devs.assign(1, device);
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  ncclResult_t r = a->init_rank(c->comms.data(), nranks, uid, rank);  // collective over the nranks processes
+  (void)hipSetDevice(prev);
+  if (r != ncclSuccess) {
+    delete c;
+    return err(FA_E_HIP, "fa_rccl_init_rank: ncclCommInitRank", r);
+  }
+  *comm_out = c;
+  return FA_OK;
+}
+
+// What RCCL reports for a handle: its rank count (ncclCommCount, the same on every communicator of the handle or
+// FA_E_HIP), and for each of the handle's communicators i its rank (ncclCommUserRank) and device
+// (ncclCommCuDevice).  `ranks` / `devs` hold one entry per communicator of the handle (fa_rccl_init: ndev;
+// fa_rccl_init_rank: 1); either may be NULL.
+extern "C" int fa_rccl_comm_info(void* comm, int32_t* count, int32_t* ranks, int32_t* devs) {
+  Comm* c;
+  int e = check(comm, 0, "fa_rccl_comm_info: bad arguments", &c);
+  if (e) return e;
+  if (!count) return fa_internal_set_error(FA_E_ARG, "fa_rccl_comm_info: NULL count");
+  const RcclApi* a = api();
+  int n0 = -1;
+  for (int i = 0; i < c->n; ++i) {
+    int n = -1, rk = -1, d = -1;
+    ncclResult_t r = a->count(c->comms[i], &n);
+    if (r == ncclSuccess) r = a->user_rank(c->comms[i], &rk);
+    if (r == ncclSuccess) r = a->cu_device(c->comms[i], &d);
+    if (r != ncclSuccess) return err(FA_E_HIP, "fa_rccl_comm_info", r);
+    if (i > 0 && n != n0) return fa_internal_set_error(FA_E_HIP, "fa_rccl_comm_info: the communicators disagree "
+                                                                  "on the rank count");
+    n0 = n;
+    if (ranks) ranks[i] = rk;
+    if (devs) devs[i] = d;
+  }
+  *count = n0;
   return FA_OK;
 }
 

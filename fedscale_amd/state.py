@@ -321,6 +321,50 @@ _LIVE_GROUPS: "set" = set()
 atexit.register(_close_live_groups)
 
 
+def comm_info(comm, n_local: int) -> dict:
+    """{count, ranks, devices} of an fa_rccl handle as RCCL reports them (fa_rccl_comm_info)."""
+    import ctypes
+
+    from . import _native
+
+    cnt = ctypes.c_int32(-1)
+    ranks = (ctypes.c_int32 * n_local)()
+    devs = (ctypes.c_int32 * n_local)()
+    _native.call("fa_rccl_comm_info", comm, ctypes.byref(cnt), ranks, devs)
+    return {"count": cnt.value, "ranks": list(ranks), "devices": list(devs)}
+
+
+def spmd_rccl_probe(device_index: int, group=None) -> dict:
+    """One process per GPU (torch.distributed initialised): open an RCCL communicator of our own over the ranks
+    (fa_rccl_unique_id on rank 0, broadcast through the process group, fa_rccl_init_rank on every rank), ask RCCL
+    for its rank count, rank and device, gather those to every rank and close it.  What a multi-GPU record shows
+    as "RCCL saw N ranks"."""
+    import ctypes
+
+    import torch.distributed as dist
+
+    from . import _native
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    idbuf = (ctypes.c_char * 128)()
+    if rank == 0:
+        _native.call("fa_rccl_unique_id", idbuf)
+    obj = [bytes(idbuf) if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    ctypes.memmove(idbuf, obj[0], 128)
+    h = ctypes.c_void_p()
+    _native.call("fa_rccl_init_rank", world, idbuf, rank, device_index, ctypes.byref(h))
+    try:
+        mine = comm_info(h, 1)
+    finally:
+        _native.call("fa_rccl_destroy", h)
+    every = [None] * world
+    dist.all_gather_object(every, (mine["count"], mine["ranks"][0], mine["devices"][0]), group=group)
+    return {"count": every[0][0], "counts_agree": all(e[0] == every[0][0] for e in every),
+            "rank_of_process": [e[1] for e in every], "device_of_rank": [e[2] for e in every],
+            "source": "fa_rccl_init_rank + fa_rccl_comm_info (ncclCommCount / ncclCommUserRank / ncclCommCuDevice)"}
+
+
 class DeviceGroup:
     """The GPUs ONE aggregator process drives (FedScale's aggregator is a single process, aggregator.py:
     177-192, 919-963).  Cross-device steps are RCCL collectives over xGMI issued for every device at once
@@ -372,6 +416,15 @@ class DeviceGroup:
             self._comm = h
             _LIVE_GROUPS.add(self)  # destroyed by close() or at interpreter exit, never by GC
         return self._comm
+
+    def rccl_info(self) -> dict:
+        """What RCCL itself reports for the group's communicator (fa_rccl_comm_info: ncclCommCount, and per
+        position ncclCommUserRank / ncclCommCuDevice); the copy transport has no communicator."""
+        if self.transport != "rccl":
+            return {"transport": self.transport, "count": None,
+                    "note": "no RCCL communicator: a device hosts several parts (copy transport)"}
+        return {"transport": "rccl", **comm_info(self._rccl(), self.world),
+                "devices_requested": [d.index for d in self.devices]}
 
     def close(self):
         if self._comm is not None:

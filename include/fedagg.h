@@ -58,6 +58,13 @@ enum {
 int fa_abi_version(void);
 const char* fa_last_error_string(void);
 
+/* Build provenance (ABI 4).  fa_build_id(): 16 hex digits of SHA-256 over the compiler flags, the extra -D
+ * definitions (fa_build_defs(), "" for the product build) and every source and header of this library
+ * (fedscale_amd/buildinfo.py).  The loader recomputes it from the tree and refuses a library that differs.
+ * No reference counterpart. */
+const char* fa_build_id(void);
+const char* fa_build_defs(void);
+
 /* What a pointer is to the GPU: 0 device memory (or NULL), 1 pinned host memory the GPU reads at the same
  * address (hipHostMalloc, torch pin_memory), -1 anything else (pageable, unregistered, managed) — no entry point
  * hands such a pointer to a kernel: fa_reduce, fa_reduce_mirror and fa_side_accumulate reject it with FA_E_ARG.
@@ -320,6 +327,18 @@ int fa_rccl_gather(void* comm, const void* const* send, void* recv_root, int64_t
                    void* const* streams);
 int fa_rccl_broadcast(void* comm, void* const* bufs, int64_t count, int32_t dtype, int32_t root,
                       void* const* streams);
+
+/* What RCCL itself reports for a handle (ABI 4): *count = ncclCommCount (every communicator of the handle must
+ * agree, else FA_E_HIP); ranks[i] = ncclCommUserRank and devs[i] = ncclCommCuDevice of the handle's i-th
+ * communicator (one per device given to fa_rccl_init; one for fa_rccl_init_rank).  ranks / devs may be NULL.
+ * The bench records it on every N > 1 line, so a multi-GPU record shows the rank count RCCL saw. */
+int fa_rccl_comm_info(void* comm, int32_t* count, int32_t* ranks, int32_t* devs);
+/* One rank of a communicator spanning processes (one process per GPU, the SPMD bench): fa_rccl_unique_id on one
+ * rank writes NCCL_UNIQUE_ID_BYTES (128) bytes the caller broadcasts; every rank then calls fa_rccl_init_rank
+ * with its rank and its device (collective: it returns once all nranks have joined).  Destroy with
+ * fa_rccl_destroy.  No reference counterpart. */
+int fa_rccl_unique_id(void* id_out);
+int fa_rccl_init_rank(int32_t nranks, const void* id, int32_t rank, int32_t device, void** comm_out);
 
 #ifdef __cplusplus
 }

@@ -439,7 +439,10 @@ def test_rccl_collectives_one_gpu(gpu_device):
     for i in range(1, 5):
         want = want + rows[i]
     assert torch.equal(o, want)
+    info = g.rccl_info()  # what RCCL itself reports (fa_rccl_comm_info)
+    assert info == {"transport": "rccl", "count": 1, "ranks": [0], "devices": [0], "devices_requested": [0]}
     g.close()
+    assert DeviceGroup([0, 0], transport="copy").rccl_info()["count"] is None
 
 
 def test_rccl_communicator_left_open_at_exit(gpu_device):
@@ -484,6 +487,11 @@ def test_nccl_process_group_collectives_world1(gpu_device):
         g.collective_all_reduce(s)
         assert torch.equal(s, torch.ones_like(s))
         assert dist.get_backend() == "nccl"
+        from fedscale_amd.state import spmd_rccl_probe
+
+        probe = spmd_rccl_probe(0)  # our own RCCL communicator over the process group's ranks
+        assert probe["count"] == 1 and probe["counts_agree"]
+        assert probe["rank_of_process"] == [0] and probe["device_of_rank"] == [0]
     finally:
         dist.destroy_process_group()
 
