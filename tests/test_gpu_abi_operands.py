@@ -216,8 +216,8 @@ def test_pageable_operand_in_every_position_is_rejected_before_any_launch(gpu_de
     torch.cuda.synchronize()
     del keep
     # every launching entry point of the ABI is covered (queries, host-only and RCCL calls are not launches)
-    host_or_query = {"fa_abi_version", "fa_last_error_string", "fa_pointer_kind", "fa_reduce_launches",
-                     "fa_qfed_launches", "fa_qfed_max_chunk", "fa_qfed_workspace_bytes", "fa_host_gather",
+    host_or_query = {"fa_abi_version", "fa_build_id", "fa_build_defs", "fa_last_error_string", "fa_pointer_kind",
+                     "fa_reduce_launches", "fa_qfed_launches", "fa_qfed_max_chunk", "fa_qfed_workspace_bytes", "fa_host_gather",
                      "fa_pickle_strip", "fa_dp_workspace_bytes", "fa_host_register", "fa_host_unregister",
                      "fa_h2d_pieces"}  # (fa_h2d_pieces: its own test below)
     rccl = {n for n in exported if n.startswith("fa_rccl_")}
