@@ -9,7 +9,8 @@ A "step" is one aggregation round over the resident K x P batch.
 
 --gpus N (one process per GPU, torchrun; RCCL over xGMI) shards THE SAME model over the ranks (strong
 scaling, the north star's "1000 x 25M ... >= 3.5x at 8 GPUs"): rank r owns the 64-aligned parameter slice
-[r*S, (r+1)*S), S = ceil(P/N) rounded up to 64, and reduces its slice of every client update — no
+[b_r, b_r+1), b_r = r*P/N rounded to a multiple of 64 (every slice within 64 floats of P/N), and
+reduces its slice of every client update — no
 data-path collective (each output element depends only on its own column).  ``value`` = K * steps / wall
 (max over ranks): client updates of the whole model per second.  The RCCL all-gather that reassembles the
 global model for egress is timed separately (``reassembly_ms``), outside ``value``.
@@ -77,6 +78,9 @@ def parse():
     ap.add_argument("--no-reassemble", action="store_true", help="skip the egress all-gather timing at N>1")
     ap.add_argument("--rest", type=float, default=None,
                     help="seconds the card idles before each heavy timed region (default %g; 0 = off)" % REST_S)
+    ap.add_argument("--sustain", type=float, default=10.0,
+                    help="N = 1: seconds of back-to-back headline rounds after the rested timed region (the sustained "
+                         "rate and the card's state; 0 = skip)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the headline CPU sample (0 = skip "
                                                                      "every CPU leg)")
     ap.add_argument("--seed", type=int, default=2024)
@@ -413,7 +417,7 @@ class Workload:
 
         from fedscale_amd import kernels as kx
         from fedscale_amd import synth
-        from fedscale_amd.bucket import round_up
+        from fedscale_amd.bucket import round_up, shard_bounds, shard_ld
 
         self.policy, self.K, self.world, self.dev, self.shards = policy, K, world, dev, shards
         self.cmode = shards.shards_clients
@@ -421,10 +425,9 @@ class Workload:
             self.P, self.P_total = P_total, P_total * (world if weak else 1)
             ld = round_up(P_total, 64)
         else:
-            S = round_up(max(1, -(-P_total // world)), 64)
-            p0 = min(P_total, rank * S)
-            self.P, self.P_total = min(P_total, p0 + S) - p0, P_total
-            ld = S
+            b = shard_bounds(P_total, world)  # the drop-in's balanced 64-aligned slices (BucketLayout)
+            self.P, self.P_total = b[rank + 1] - b[rank], P_total
+            ld = shard_ld(P_total, world)
         self.ld = ld
         free, _ = torch.cuda.mem_get_info(dev)
         cap = max(1, int(free * budget_fraction) // (4 * ld * sets))
@@ -588,6 +591,20 @@ def _all_ranks(val: float, dev, world, backend) -> list:
     return [float(o.cpu()[0]) for o in out]
 
 
+def pmc_traffic(workload: str, resident: int, launches: int, build_id: str, path: str = None):
+    """roofline.traffic: HBM bytes per launch of THIS run's shape and library, from profiles/pmc_traffic.json
+    (tools/pmc_parse.py keys every entry by workload, resident clients per pass, launches per round and the build
+    id of the library the profiled command loaded).  None when no entry has all four."""
+    path = path or PMC_FILE
+    try:
+        with open(path) as f:
+            db = json.load(f)
+    except (OSError, ValueError):
+        return None
+    e = db.get("entries", {}).get(f"{workload}|C{resident}|L{launches}|{build_id}")
+    return None if e is None else float(e["hbm_bytes_per_launch"])
+
+
 #: seconds the card idles before each heavy timed region (--rest).  A FedScale aggregator's GPU works in bursts: one
 #: reduction per round, idle while the clients train.  After minutes of back-to-back streaming the same launches run
 #: 3-4 % slower (the card's power/thermal state, not the allocation history: tools/inline_probe.py,
@@ -617,12 +634,18 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend):
         w.step()
     split = w.yogi is not None and not w.cmode  # FedYoGi: a third event between the mean and the YoGi step
     evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3 if split else 2)) for _ in range(steps)]
+    from fedscale_amd.cardstate import CardSampler
+
+    w.card_before = CardSampler(dev).read_once()
+    sampler = CardSampler(dev, period_s=0.02)
     _sync_all(dev, world)
+    sampler.start()
     t0 = time.perf_counter()
     for i in range(steps):
         w.step(evs[i])
     _sync_all(dev, world)
     wall = time.perf_counter() - t0
+    w.card = sampler.stop().summary()
     kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
     w.split_ms = None
     if split:  # (mean of k_reduce's launches, mean of k_yogi_step) per step, max over ranks
@@ -756,7 +779,33 @@ def run_selfcheck(world: int, timeout_s: int = 150) -> dict:
     return out
 
 
-def run_inproc_bench(world: int, K: int, P: int, backend: str, timeout_s: int = 240) -> dict:
+def promote_inproc(res: dict, inproc: dict, K: int, steps: int) -> None:
+    """N > 1: the line's ``value`` is the in-process drop-in's round (one aggregator process driving the N GPUs,
+    ShardedModelAdapter: what a FedScale deployment runs, aggregator.py:177-192 / 919-963), timed over the same
+    ``steps`` after the same warmup, every part's launches included, from the first launch to every part's last
+    kernel.  The SPMD figure (one process per GPU) stays beside it as ``value_spmd``.  If the in-process run failed,
+    ``value`` stays the SPMD one and ``value_source`` says why."""
+    fa = inproc.get("policies", {}).get("fedavg") if "policies" in inproc else inproc
+    if not fa or not fa.get("ok") or "inproc_round_ms" not in fa:
+        res["value_source"] = "spmd (the in-process drop-in run failed: %s)" % ((fa or inproc).get("error"),)
+        return
+    res["value_spmd"], res["ms_per_step_spmd"] = res["value"], res["ms_per_step"]
+    if "scaling_vs_one_gpu" in res:
+        res["scaling_vs_one_gpu_spmd"] = res.pop("scaling_vs_one_gpu")
+    ms = fa["inproc_round_ms"]
+    res["ms_per_step"] = ms
+    res["value"] = K / (ms * 1e-3)
+    res["value_source"] = ("inproc_drop_in.fedavg: one process, ShardedModelAdapter over the N GPUs, %d timed rounds "
+                           "after the same warmup (synchronize on every GPU both sides)" % fa.get("rounds", steps))
+    if "speedup_vs_one_gpu" in fa:
+        res["scaling_vs_one_gpu"] = fa["speedup_vs_one_gpu"]
+    res["config"]["parallelism"] = (f"param-shard x{len(fa['devices'])} in ONE aggregator process "
+                                    f"(ShardedModelAdapter, transport {fa.get('transport')}); value_spmd: one process "
+                                    "per GPU")
+
+
+def run_inproc_bench(world: int, K: int, P: int, backend: str, steps: int = 6, warmup: int = 2,
+                     timeout_s: int = 300) -> dict:
     """fedscale_amd.inproc_bench in a child process (rank 0, N > 1): a timed device-resident round of the
     in-process drop-in (ShardedModelAdapter over GPUs 0..N-1, the way FedScale's single-process aggregator is
     deployed on a node) beside the single-device adapter.  With fewer GPUs than ranks (a gloo rehearsal on one
@@ -768,7 +817,8 @@ def run_inproc_bench(world: int, K: int, P: int, backend: str, timeout_s: int = 
     nd = torch.cuda.device_count()
     devs = [i % max(1, nd) for i in range(world)]
     cmd = [sys.executable, "-m", "fedscale_amd.inproc_bench", "--devices", ",".join(map(str, devs)),
-           "--clients", str(K), "--params", str(P), "--policies", "fedavg,fed-yogi"]
+           "--clients", str(K), "--params", str(P), "--policies", "fedavg,fed-yogi", "--rounds", str(steps),
+           "--warmup", str(warmup)]
     t0 = time.perf_counter()
     try:
         r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout_s)
@@ -807,6 +857,51 @@ def one_gpu_reference(policy, K, P, dev, seed, steps=5, warmup=2) -> dict:
     return {"ms_per_step": ms, "client_updates_per_s": K / (ms * 1e-3), "steps": steps}
 
 
+def sustained_leg(w: "Workload", dev, seconds: float, launches: int, est_ms: float, window_s: float = 3.0) -> dict:
+    """Back-to-back rounds of the headline workload for ``seconds`` right after its rested timed region, no rest:
+    the rate a card streaming without pause settles at, beside the card's power, temperatures and clocks (sysfs,
+    fedscale_amd/cardstate.py).  Chunks of ~1 s, each timed by one HIP event pair on the launch stream;
+    ``sustained`` = the chunks of the last ``window_s`` seconds."""
+    import numpy as np
+    import torch
+
+    from fedscale_amd.cardstate import CardSampler
+
+    per_chunk = max(1, int(round(1000.0 / max(est_ms, 1e-3))))
+    sampler = CardSampler(dev, period_s=0.05)
+    torch.cuda.synchronize(dev)
+    sampler.start()
+    t_start = time.perf_counter()
+    chunks = []
+    while time.perf_counter() - t_start < seconds:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0 = time.perf_counter()
+        e0.record(w.stream)
+        for _ in range(per_chunk):
+            w.step()
+        e1.record(w.stream)
+        torch.cuda.synchronize(dev)
+        chunks.append((t0, time.perf_counter(), per_chunk, e0.elapsed_time(e1) / per_chunk))
+    sampler.stop()
+    alg = w.alg_bytes
+    keys = ("power_w", "temp_junction_c", "temp_mem_c", "sclk_mhz", "mclk_mhz")
+    series = []
+    for t0, t1, n, ms in chunks:
+        card = sampler.summary(t0, t1)
+        series.append(dict({"t_s": round(t0 - t_start, 2), "steps": n, "ms_per_step": ms,
+                            "hbm_gbps": alg / (ms * 1e-3) / 1e9},
+                           **{k: card[k]["mean"] for k in keys if k in card}))
+    t_end = chunks[-1][1]
+    last = [c for c in chunks if c[0] >= t_end - window_s] or chunks[-1:]
+    ms = float(np.sum([c[2] * c[3] for c in last]) / np.sum([c[2] for c in last]))
+    gbps = alg / (ms * 1e-3) / 1e9
+    return {"seconds": round(t_end - t_start, 2), "window_s": window_s, "steps": int(sum(c[2] for c in chunks)),
+            "ms_per_step": ms, "ms_per_launch": ms / launches, "hbm_gbps": gbps, "frac": gbps / HBM_PEAK_GBS,
+            "card_window": sampler.summary(last[0][0], t_end), "series": series,
+            "note": ("back-to-back headline rounds right after the rested timed region, no rest: the last %g s of "
+                     "%g s; one HIP event pair per ~1 s chunk on the launch stream" % (window_s, round(t_end - t_start, 1)))}
+
+
 def main():
     global REST_S
     args = parse()
@@ -828,11 +923,16 @@ def main():
     from fedscale_amd.hostnuma import bind_to_gpu
 
     numa_node = bind_to_gpu(dev)
+    cpu_group = None
     if world > 1:
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
+            cpu_group = dist.new_group(backend="gloo")  # host-side waits (no kernel parked on the GPUs)
         else:
             dist.init_process_group("gloo")
+    from fedscale_amd import _native
+
+    _native.load()  # refuses a library not built from this tree's sources (fedscale_amd/buildinfo.py)
     from fedscale_amd.state import ShardGroup
 
     shards = ShardGroup(rank, world, mode=args.shard)
@@ -848,6 +948,18 @@ def main():
                                                                  args.dist_backend)
     pg_world = dist.get_world_size() if world > 1 else 1
     strong = not weak and not w.cmode
+    card_state = {"before_timed_region": w.card_before, "timed_region": w.card, "rest_s": w.rest_s}
+    from fedscale_amd import kernels as kx
+    if policy == "qfedavg":
+        launches = len(w.passes) * kx.qfed_launches(w.ld, w.P, chain=bool(w.qf.get("chain") is not None))
+    else:
+        launches = len(w.passes) * kx.reduce_launches(w.C if len(w.passes) > 1 else K, w.P,
+                                                      weighted=policy == "fedbuff")
+        if policy == "fedyogi":
+            launches += 1  # k_yogi_step after the mean
+    sustained = None
+    if world == 1 and args.sustain > 0:
+        sustained = sustained_leg(w, dev, args.sustain, launches, wall * 1e3 / args.steps)
 
     reassembly_ms = None
     if world > 1 and not args.no_reassemble and not w.cmode:  # egress: rebuild the global model (RCCL)
@@ -858,20 +970,23 @@ def main():
             shards.collective_all_gather(w.out)
         torch.cuda.synchronize(dev)
         reassembly_ms = _max_over_ranks([(time.perf_counter() - t0r) * 1e3 / 5], dev, world, args.dist_backend)[0]
+    rccl_probe = None
+    if world > 1:  # what RCCL itself sees over the ranks (its own communicator; ranks sharing a GPU cannot open one)
+        if args.dist_backend == "nccl":
+            from fedscale_amd.state import spmd_rccl_probe
+
+            try:
+                rccl_probe = spmd_rccl_probe(local_dev)
+            except Exception as e:  # reported, never fatal
+                rccl_probe = {"error": f"{type(e).__name__}: {e}"}
+        else:
+            rccl_probe = {"skipped": "gloo rehearsal: the ranks share one GPU, RCCL takes one rank per GPU"}
     alg_bytes = w.alg_bytes
     P_local, n_passes = w.P, len(w.passes)
-    w_chain = bool(getattr(w, "qf", None) and w.qf.get("chain") is not None)
-    w_ld = w.ld
+    resident = w.C
     split_ms = getattr(w, "split_ms", None)  # FedYoGi: (k_reduce ms, k_yogi_step ms) per step
-    # launches of the dominant kernel per step: fa_reduce runs long buckets as column windows (fedagg.hip
-    # FA_WINDOWS), so the per-launch figures rocprof reports are the step's divided by this
-    from fedscale_amd import kernels as kx
-    if policy == "qfedavg":
-        launches = n_passes * kx.qfed_launches(w_ld, P_local, chain=w_chain)
-    else:
-        launches = n_passes * kx.reduce_launches(w.C if n_passes > 1 else K, P_local, weighted=policy == "fedbuff")
-        if policy == "fedyogi":
-            launches += 1  # k_yogi_step after the mean
+    # (launches: of the dominant kernel per step; fa_reduce runs long buckets as column windows (fedagg.hip
+    # FA_WINDOWS), so the per-launch figures rocprof reports are the step's divided by it)
     w.free()
     del w
 
@@ -888,14 +1003,17 @@ def main():
 
     one_gpu = inproc = None
     if world > 1 and strong and not args.no_selfcheck:
-        # outside the timed region, the other ranks waiting at the barrier: (1) the same round on one GPU over the
+        # outside the timed region, the other ranks waiting at a host-side barrier (gloo: an RCCL barrier would park
+        # a spinning kernel on their GPUs while rank 0's child uses them): (1) the same round on one GPU over the
         # whole model, so the line carries its own scaling reference; (2) the in-process drop-in timed over the
-        # node's GPUs (what a FedScale deployment runs: one aggregator process)
+        # node's GPUs — what a FedScale deployment runs (one aggregator process), and the N > 1 line's `value`
         _sync_all(dev, world)
+        dist.barrier(group=cpu_group)
         if rank == 0:
             one_gpu = one_gpu_reference(policy, K, P, dev, args.seed)
-            inproc = run_inproc_bench(world, K, P, args.dist_backend) if policy == "fedavg" else None
-        dist.barrier()
+            if policy == "fedavg":
+                inproc = run_inproc_bench(world, K, P, args.dist_backend, steps=args.steps, warmup=args.warmup)
+        dist.barrier(group=cpu_group)
 
     selfcheck = None
     if world > 1 and not args.no_selfcheck and args.dist_backend == "nccl":
@@ -903,9 +1021,10 @@ def main():
         # one-GPU box cannot run.  A child process with a deadline, after every rank has freed its workloads;
         # the other ranks wait at the barrier.  Outside the timed region; reported, never fatal.
         _sync_all(dev, world)
+        dist.barrier(group=cpu_group)
         if rank == 0:
             selfcheck = run_selfcheck(world)
-        dist.barrier()
+        dist.barrier(group=cpu_group)
 
     if rank == 0:
         ms_per_step = wall * 1e3 / args.steps
@@ -913,15 +1032,6 @@ def main():
         # the slowest rank's kernel sets the job's pace: roofline from the max over ranks (rank 0's slice is the
         # largest, so bytes / max time is the conservative per-GPU rate); N = 1: the same number
         achieved = alg_bytes / (kern_ms_max * 1e-3) / 1e9
-        traffic = None
-        if os.path.exists(PMC_FILE):
-            try:
-                pmc = json.load(open(PMC_FILE))
-                key = f"{policy}_k{K}_p{P_local}"
-                if key in pmc:
-                    traffic = pmc[key]["hbm_bytes_per_launch"]
-            except Exception:
-                traffic = None
         w_cmode = shards.shards_clients
         if w_cmode:
             config = {"workload": f"{policy}_k{K}_per_gpu_p{P}_clientshard", "clients": K * world,
@@ -937,6 +1047,7 @@ def main():
                       "parallelism": f"param-shard x{world} (one process per GPU, no data-path collective)"}
         if n_passes > 1:
             config["streamed_passes"] = n_passes
+        build_id = _native.build_info()["build_id"]
         res = {
             "metric": ("client-updates/sec + HBM GB/s, device-resident FedAvg reduce of KxP fp32"
                        if policy == "fedavg" else
@@ -947,26 +1058,33 @@ def main():
             "data": "synthetic full-weight client updates (base + noise, hash-generated on device), HBM-resident",
             "host_numa_node": numa_node,
             "card_rest_s": REST_S,
+            "build_id": build_id,
             "config": config,
             "hbm_gbps": achieved,
             "kernel_ms": kern_ms_max,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "frac": achieved / HBM_PEAK_GBS,
+                         "traffic": pmc_traffic(config["workload"], resident, launches, build_id),
                          "kernel": ("k_qfed_accum + k_qfed_gather (fa_qfed_accumulate)" if policy == "qfedavg"
                                     else "k_reduce (fa_reduce, this rank's partial chain)" if w_cmode else
                                     {"fedavg": "k_reduce (fa_reduce FA_FINALIZE)",
                                      "fedbuff": "k_reduce weighted (fa_reduce FA_FINALIZE)",
                                      "fedyogi": "k_reduce (fa_reduce FA_FINALIZE) + k_yogi_step"}[policy]),
                          "alg_bytes_per_launch": alg_bytes / launches, "launches_per_step": launches,
-                         "kernel_ms_per_launch": kern_ms_max / launches},
+                         "resident_clients": resident, "kernel_ms_per_launch": kern_ms_max / launches,
+                         "traffic_key": "profiles/pmc_traffic.json entries[workload|C<resident_clients>|"
+                                        "L<launches_per_step>|<build_id>] (null: no PMC pass of this shape and build)"},
+            "card_state": card_state,
         }
+        if sustained is not None:
+            res["sustained"] = sustained
         if split_ms:
             res["roofline"]["kernel_ms_split"] = {"k_reduce": split_ms[0], "k_yogi_step": split_ms[1],
                                                   "k_reduce_launches": launches - 1}
         if world > 1:  # self-checking SCALE records: every rank's kernel time and the process group's size
             res["ranks"] = {"world_process_group": pg_world, "backend": args.dist_backend,
                             "kernel_ms_per_rank": kern_ms_ranks, "kernel_ms_max": kern_ms_max,
-                            "kernel_ms_rank0": kern_ms,
+                            "kernel_ms_rank0": kern_ms, "rccl": rccl_probe,
                             "roofline_from": "max over ranks of the dominant kernel's mean time per step"}
         if reassembly_ms is not None:
             # every round ends in egress (aggregator.py:788-804): the model reassembled from the shards
@@ -980,6 +1098,7 @@ def main():
                 res["scaling_vs_one_gpu_incl_reassembly"] = one_gpu["ms_per_step"] / (ms_per_step + reassembly_ms)
         if inproc is not None:
             res["inproc_drop_in"] = inproc
+            promote_inproc(res, inproc, K, args.steps)
         if selfcheck is not None:
             res["inproc_multi_gpu_check"] = selfcheck
         if other is not None:
@@ -990,7 +1109,7 @@ def main():
             res["cpu_baseline"] = None
         print(json.dumps(res), flush=True)
     if world > 1:
-        dist.barrier()
+        dist.barrier(group=cpu_group)
         dist.destroy_process_group()
 
 

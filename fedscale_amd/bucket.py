@@ -2,9 +2,10 @@
 
 HBM layout:
   * fp32 entries of the state_dict, concatenated in state_dict order -> one flat vector of P elements.
-    A rank owns the contiguous slice [p0, p1) of it (balanced, 64-element aligned, equal-size shards so
-    the reassembly is a plain all-gather); its local row stride ``ld`` is P_local rounded up to 64
-    floats (256 B) and the padding is kept at zero.
+    A rank owns the contiguous slice [p0, p1) of it: the boundaries are r*P/N rounded to the nearest
+    multiple of 64, so every slice starts 256-byte aligned and holds P/N floats within 64 (shard_bounds).
+    Every rank's row stride ``ld`` is the same (the largest slice rounded up to 64 floats) and the padding is
+    kept at zero, so the reassembly is a plain all-gather of ld floats per rank followed by unshard().
   * non-fp32 entries (int64 BatchNorm ``num_batches_tracked`` ...) -> the "side table" of Q int64
     elements, replicated on every rank (it is a few hundred bytes).
   * a round's client updates live client-major: x[slot, :] (fp32, [capacity, ld]) and xi[slot, :]
@@ -49,6 +50,26 @@ def round_up(n: int, m: int) -> int:
     return (n + m - 1) // m * m
 
 
+def shard_bounds(P: int, world: int) -> List[int]:
+    """[b_0 = 0, b_1, ..., b_world = P]: b_r = r*P/world rounded to the nearest multiple of ALIGN (ties down), so
+    every slice [b_r, b_r+1) starts 64-float aligned and |slice - P/world| <= 64 (each boundary is within 32 of
+    its ideal).  Rounds 1-4 cut equal slices of round_up(ceil(P/world), 64), which left the last one up to
+    64*(world-1) floats short (256 at 100 M over 8)."""
+    if world < 1:
+        raise ValueError("world >= 1")
+    b = [0]
+    for r in range(1, world):
+        b.append(min(P, max(b[-1], ((2 * r * P + ALIGN * world - 1) // (2 * ALIGN * world)) * ALIGN)))
+    b.append(P)
+    return b
+
+
+def shard_ld(P: int, world: int) -> int:
+    """The row stride every rank of a P-float model over ``world`` uses: the largest slice, rounded up to 64."""
+    b = shard_bounds(P, world)
+    return max(ALIGN, round_up(max(b[r + 1] - b[r] for r in range(world)), ALIGN))
+
+
 @dataclass
 class Entry:
     index: int
@@ -89,11 +110,10 @@ class BucketLayout:
         self.P_full = pf
         self.Q = pi
         self.rank, self.world = rank, world
-        self.shard = round_up(max(1, -(-pf // world)), ALIGN)  # equal-size shards
-        self.p0 = min(pf, rank * self.shard)
-        self.p1 = min(pf, self.p0 + self.shard)
+        self.bounds = shard_bounds(pf, world)  # balanced, 64-aligned slice boundaries
+        self.p0, self.p1 = self.bounds[rank], self.bounds[rank + 1]
         self.P = self.p1 - self.p0
-        self.ld = self.shard  # local row stride (multiple of 64, >= P)
+        self.ld = shard_ld(pf, world)  # row stride of every rank (multiple of 64, >= every P)
         self.ldq = max(1, self.Q)
         self.f_entries = [e for e in self.entries if e.kind == "f"]
         self.i_entries = [e for e in self.entries if e.kind == "i"]
@@ -112,6 +132,17 @@ class BucketLayout:
             self._gather_entries.append((e.index, e.name, e.shape, e.kind, src, e.offset))
         self._gather_offs = np.asarray(offs, dtype=np.int64)
         self._gather_sizes = np.asarray(sizes, dtype=np.int64)
+
+    def unshard(self, gathered):
+        """The P_full-float model from an all-gather of every rank's ld-float row (rank r's slice is the first
+        P_r floats of row r): a view when the slices fill their rows, else one compaction copy (torch or numpy)."""
+        if self.world == 1:
+            return gathered[:self.P_full]
+        ld, b = self.ld, self.bounds
+        if all(b[r + 1] - b[r] == ld for r in range(self.world - 1)):
+            return gathered[:self.P_full]
+        parts = [gathered[r * ld:r * ld + (b[r + 1] - b[r])] for r in range(self.world)]
+        return torch.cat(parts) if isinstance(gathered, torch.Tensor) else np.concatenate(parts)
 
     @classmethod
     def from_state_dict(cls, sd, rank: int = 0, world: int = 1) -> "BucketLayout":

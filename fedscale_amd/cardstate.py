@@ -88,7 +88,8 @@ class CardSampler:
         self._t = None
         self.t0 = self.t1 = None
 
-    def sample(self):
+    def _one(self) -> dict:
+        out = {}
         for k, (path, conv) in self.files.items():
             t = _read(path)
             if t is None:
@@ -98,7 +99,20 @@ class CardSampler:
             except ValueError:
                 v = None
             if v is not None:
-                self.samples[k].append(v)
+                out[k] = v
+        return out
+
+    def sample(self):
+        now = time.perf_counter()
+        for k, v in self._one().items():
+            self.samples[k].append((now, v))
+
+    def read_once(self) -> dict:
+        """One reading of every source, not stored (the card's state before a region)."""
+        out = self._one()
+        if self.missing:
+            out["missing"] = list(self.missing)
+        return out
 
     def _run(self):
         while not self._stop.is_set():
@@ -126,10 +140,15 @@ class CardSampler:
         self.stop()
         return False
 
-    def summary(self) -> dict:
-        out = {"seconds": round((self.t1 or time.perf_counter()) - (self.t0 or 0), 3), "source": self.pci}
+    def summary(self, t_from: float = None, t_to: float = None) -> dict:
+        """mean / min / max / median / last of every source over the samples in [t_from, t_to] (perf_counter
+        seconds; default: the whole run)."""
+        lo = self.t0 if t_from is None else t_from
+        hi = (self.t1 or time.perf_counter()) if t_to is None else t_to
+        out = {"seconds": round(hi - (lo or hi), 3), "source": self.pci}
         n = 0
-        for k, vs in self.samples.items():
+        for k, tv in self.samples.items():
+            vs = [v for t, v in tv if (t_from is None or t >= t_from) and (t_to is None or t <= t_to)]
             if not vs:
                 continue
             n = max(n, len(vs))
@@ -144,6 +163,4 @@ class CardSampler:
 
 def snapshot(dev) -> dict:
     """One reading of every source (the card's state before a region)."""
-    s = CardSampler(dev)
-    s.sample()
-    return {k: v[0] for k, v in s.samples.items() if v} | ({"missing": s.missing} if s.missing else {})
+    return CardSampler(dev).read_once()

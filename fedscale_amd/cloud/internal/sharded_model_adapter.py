@@ -102,8 +102,8 @@ class ShardedModelAdapter(TorchModelAdapter):
         self._next_row = 0
         self._regs = {}  # registered address -> [payload object, events of the copies out of it]
         self._reg_segs = None
-        self._reg_failed = False
         self.registered_uploads = 0  # uploads staged out of their registered payload (the rest: pinned-row gather)
+        self.registration_fallbacks = 0  # qualifying uploads that took the gather (page shared / register refused)
         self.pack_workers = default_pack_workers()
         self._init_egress(True)
         self._egress_src = self._part_buffers()
@@ -158,7 +158,7 @@ class ShardedModelAdapter(TorchModelAdapter):
         host buffer that is (or now gets) registered; None: take the pinned-row gather."""
         from ... import _native
 
-        if self.REGISTER_MIN_ENTRY_BYTES < 0 or self._reg_failed:
+        if self.REGISTER_MIN_ENTRY_BYTES < 0:
             return None
         if self._reg_segs is None:
             self._reg_segs = PieceSegments(self.layout, self.REGISTER_MIN_ENTRY_BYTES)
@@ -172,7 +172,14 @@ class ShardedModelAdapter(TorchModelAdapter):
             while isinstance(r.base, np.ndarray):
                 r = r.base
             r = r.base
-            if r is None or (root is not None and r is not root):
+            # Only an IMMUTABLE payload may be read after on_result returns (the copy engine reads the registered
+            # buffer asynchronously): the gRPC payload's bytes, or a read-only view of bytes (np.frombuffer wraps
+            # each such view in a memoryview of its own, so the bytes object is the identity).  A bytearray,
+            # writable memoryview, mmap or numpy-owned buffer the caller could reuse takes the pinned-row gather,
+            # which has copied everything before add returns, as the reference's copy at add time does.
+            if type(r) is memoryview and r.readonly and type(r.obj) is bytes:
+                r = r.obj
+            if type(r) is not bytes or (root is not None and r is not root):
                 return None
             root = r
         try:
@@ -184,14 +191,19 @@ class ShardedModelAdapter(TorchModelAdapter):
         a0, a1 = lo // page * page, -(-(lo + n) // page) * page  # whole pages of the payload's own mapping
         self._release_registrations(block=False)
         if a0 not in self._regs:
+            # two payloads next to each other on the heap can share a boundary page, and a range already registered
+            # cannot be registered again: this upload takes the gather, the next ones are tried afresh
+            if any(b0 < a1 and a0 < b1 for b0, (_, _, b1) in self._regs.items()):
+                self.registration_fallbacks += 1
+                return None
             if len(self._regs) >= self.REGISTER_MAX_PENDING:
                 self._release_registrations(block=True, keep=self.REGISTER_MAX_PENDING - 1)
             try:
                 _native.call("fa_host_register", a0, a1 - a0)
             except _native.FedAggError:
-                self._reg_failed = True  # e.g. memory the runtime will not pin: the gather from now on
+                self.registration_fallbacks += 1  # e.g. memory the runtime will not pin: this upload only
                 return None
-            self._regs[a0] = [root, []]
+            self._regs[a0] = [root, [], a1]
         return segs, np.asarray([ps[j] for j in segs.large_pieces], dtype=np.uint64), a0
 
     def _release_registrations(self, block: bool, keep: int = 0):

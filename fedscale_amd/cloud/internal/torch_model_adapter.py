@@ -266,10 +266,11 @@ class TorchModelAdapter(ModelAdapterBase):
         with es:  # its own stream, ordered after the round's kernels by an event: one host wait, at the end
             es.stream.wait_event(self._ready)
             full = self.shards.all_gather(self._f[self._cur])
+            full = L.unshard(full) if self.shards.shards_params else full[:L.P_full]
             if L.P_full == f_cpu.numel():  # (a _HostBuf holds exactly P_full floats, at least one)
-                f_cpu.copy_(full[:L.P_full], non_blocking=True)
+                f_cpu.copy_(full, non_blocking=True)
             else:
-                f_cpu[:L.P_full].copy_(full[:L.P_full], non_blocking=True)
+                f_cpu[:L.P_full].copy_(full, non_blocking=True)
             if L.Q:
                 s_cpu[:L.Q].copy_(self._s[self._cur][:L.Q], non_blocking=True)
             es.stream.synchronize()
@@ -520,7 +521,8 @@ class TorchModelAdapter(ModelAdapterBase):
             mean_f, mean_s = self._mean_device()
             L = self.layout
             full = self.shards.all_gather(mean_f[:L.ld])
-            return self._mean_lists(full[:L.P_full].to("cpu").numpy(), mean_s[:L.Q].to("cpu").numpy())
+            full = L.unshard(full) if self.shards.shards_params else full[:L.P_full]
+            return self._mean_lists(full.to("cpu").numpy(), mean_s[:L.Q].to("cpu").numpy())
 
     def _mean_lists(self, f_cpu, s_cpu) -> list:
         out = []

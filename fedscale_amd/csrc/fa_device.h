@@ -104,6 +104,7 @@ class DevScope {
 
   int rc() const { return rc_; }
   int device() const { return dev_; }
+  int unranged() const { return unranged_; }
 
   // Operand check (round 4): every buffer a launch of this call dereferences must be DEVICE memory of the
   // scope's device, or — only where the header allows it (host_ok) — pinned host memory the GPU reads at
@@ -148,8 +149,12 @@ class DevScope {
     void* base = nullptr;
     size_t size = 0;
     if (hipMemGetAddressRange((hipDeviceptr_t*)&base, &size, (hipDeviceptr_t)p) != hipSuccess || !base) {
+      // The type and device checks above have passed: the pointer IS memory of this GPU (or mapped pinned memory
+      // where the header allows it).  HIP reports no range for some allocators (hipHostRegister'd memory, VMM /
+      // expandable segments), so only the extent check is skipped here; nothing is cached for this pointer.
       (void)hipGetLastError();
-      return operr(name, "%s: no allocation range for the pointer", 0);
+      ++unranged_;
+      return FA_OK;
     }
     const Range r{(uintptr_t)base, (uintptr_t)base + size, host};
     if (a < r.lo || a >= r.hi) return operr(name, "%s lies outside the allocation HIP reports for it", 0);
@@ -229,6 +234,7 @@ class DevScope {
   static constexpr int kRanges = 16;
   Range rng_[kRanges] = {};
   int nr_ = 0, last_ = 0;
+  int unranged_ = 0;  // operands accepted without an extent check (HIP reported no range)
   const char* what_ = "";
   int prev_ = -1, dev_ = -1, saved_ = -1, rc_ = FA_OK;
 };

@@ -872,7 +872,7 @@ static_assert(QF_G == 8 || QF_G == 4, "QF_G must be 4 or 8");
 #define QF_GRID 256  // one workgroup per CU at 1 wave/SIMD (profiles/r01_tune_qfed.log)
 #endif
 #ifndef QF_CHAIN_GRID
-#define QF_CHAIN_GRID QF_GRID  // the chain launches' grid (their 8-float4 tiles leave room for 2 workgroups per CU)
+#define QF_CHAIN_GRID QF_GRID  // the chain launches' grid (one workgroup per CU: 96 KiB of LDS each at QF_MAXK 2048)
 #endif
 static_assert(QF_GRID % 16 == 0 && QF_CHAIN_GRID % 16 == 0, "the norm gathers sum the grid's rows in 16 segments");
 // workgroups of a k_qfed_accum launch (fixed per kind, so the fp64 norm order is the same on every run and device)
@@ -888,7 +888,7 @@ static inline int qf_grid(bool chain) { return chain ? QF_CHAIN_GRID : QF_GRID; 
 #ifndef QF_MAXK
 #define QF_MAXK 2048
 #endif
-static_assert(QF_MAXK % 4 == 0 && QF_MAXK <= 4096, "QF_MAXK: a multiple of 4, <= 4096 (LDS)");
+static_assert(QF_MAXK % 4 == 0, "QF_MAXK: a multiple of 4 (its LDS bound is checked per kernel variant)");
 
 struct QfArgs {
   const float* x;
@@ -1014,8 +1014,11 @@ __global__ __launch_bounds__(256, QF_MINW) void k_qfed_accum(QfArgs q) {
                 "GLDS: 0, 1 or 2 LDS slices per wave (2: 16 or 12 float4 per lane)");
   constexpr int NB = GLDS > 0 ? GLDS : 1;
   // ONE static LDS array, so it sits at LDS offset 0: the row slices first (the DMA addresses them from
-  // offset 0), then the per-client squared norms sq[4][QF_MAXK].  GLDS 2: 128 KiB + 32 KiB = 160 KiB.
+  // offset 0), then the per-client squared norms sq[4][QF_MAXK] (64 KiB at QF_MAXK 2048).  The chain launches
+  // (GLDS 1, QV 8): 32 KiB + 64 KiB = 96 KiB, one workgroup per CU.
   constexpr int ROWB = GLDS > 0 ? GLDS * 4 * QV * 64 : 0;  // f4 elements of row slices
+  static_assert(ROWB * 16 + 4 * QF_MAXK * 8 <= 160 * 1024,
+                "k_qfed_accum: row slices + per-client norms exceed gfx950's 160 KiB of LDS (GLDS / QV / QF_MAXK)");
   __shared__ f4 lds_all[ROWB + 4 * QF_MAXK / 2];
   f4* const rowbuf = lds_all;
   double(*const sq)[QF_MAXK] = reinterpret_cast<double(*)[QF_MAXK]>(lds_all + ROWB);

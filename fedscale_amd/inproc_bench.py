@@ -102,6 +102,27 @@ def _time_rounds(adapter, parts_streams, K: int, rounds: int, warmup: int) -> di
             "round_ms_incl_egress": float(np.median(both)) * 1e3}
 
 
+def _time_all_gather(group, ld: int, reps: int = 5) -> float:
+    """ms of one RCCL all-gather of the model's N slices (ld fp32 each) to every GPU over xGMI (the device-side
+    reassembly an egress could use; the drop-in's egress copies each part D2H instead)."""
+    import torch
+
+    parts, outs = [], []
+    for ds in group.streams:
+        with ds:
+            parts.append(torch.zeros(ld, dtype=torch.float32, device=ds.device))
+            outs.append(torch.empty(group.world * ld, dtype=torch.float32, device=ds.device))
+    group.all_gather(parts, outs)  # warm
+    for ds in group.streams:
+        torch.cuda.synchronize(ds.device)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        group.all_gather(parts, outs)
+    for ds in group.streams:
+        torch.cuda.synchronize(ds.device)
+    return (time.perf_counter() - t0) * 1e3 / reps
+
+
 def run(devices, K: int = 1000, P: int = 25_000_000, rounds: int = 6, warmup: int = 2, seed: int = 2024,
         one_gpu: bool = True, policy: str = "fedavg") -> dict:
     """``policy``: "fedavg" (the headline) or "fed-yogi" (config 4: the mean, then the YoGi step on every part).
@@ -125,11 +146,15 @@ def run(devices, K: int = 1000, P: int = 25_000_000, rounds: int = 6, warmup: in
             with p.dstream:  # the part's own device and stream
                 synth.fill(r.staging.x, K, p.layout.P, seed=seed + 7919 * i)
         r = _time_rounds(ad, [p.dstream for p in ad.parts], K, rounds, warmup)
-        out.update({"inproc_round_ms": r["round_ms"], "part_kernel_ms": r["part_kernel_ms"],
-                    "params_per_part": [p.layout.P for p in ad.parts],
+        out.update({"inproc_round_ms": r["round_ms"], "part_kernel_ms": r["part_kernel_ms"], "rounds": rounds,
+                    "warmup": warmup, "params_per_part": [p.layout.P for p in ad.parts],
                     "client_updates_per_s": K / (r["round_ms"] * 1e-3),
                     "hbm_gbps_aggregate": alg / (r["round_ms"] * 1e-3) / 1e9,
                     "egress_ms": r["egress_ms"], "inproc_round_ms_incl_egress": r["round_ms_incl_egress"]})
+        if policy == "fedavg":
+            out["rccl"] = ad.group.rccl_info()  # what RCCL itself reports for the group's communicator
+            if ad.group.transport == "rccl":
+                out["rccl"]["all_gather_model_ms"] = _time_all_gather(ad.group, max(p.layout.ld for p in ad.parts))
     finally:
         ad.close()
         del ad
@@ -161,6 +186,7 @@ def main(argv=None):
     p.add_argument("--clients", type=int, default=1000)
     p.add_argument("--params", type=int, default=25_000_000)
     p.add_argument("--rounds", type=int, default=6)
+    p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--no-one-gpu", action="store_true")
     p.add_argument("--policies", default="fedavg", help="comma-separated: fedavg, fed-yogi")
     a = p.parse_args(argv)
@@ -168,7 +194,8 @@ def main(argv=None):
     reps = {}
     for pol in [x.strip() for x in a.policies.split(",") if x.strip()]:
         try:
-            r = run(devices, K=a.clients, P=a.params, rounds=a.rounds, one_gpu=not a.no_one_gpu, policy=pol)
+            r = run(devices, K=a.clients, P=a.params, rounds=a.rounds, warmup=a.warmup, one_gpu=not a.no_one_gpu,
+                    policy=pol)
             r["ok"] = True
         except Exception as e:  # reported, not raised: bench.py records the failure
             r = {"devices": devices, "policy": pol, "ok": False, "error": f"{type(e).__name__}: {e}"}

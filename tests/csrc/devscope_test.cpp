@@ -110,6 +110,24 @@ int main() {
   rc = entry_reduce(x0 + ld, K - 1, ld, P, a0, out0, s0);
   expect(rc == FA_OK, "interior pointer inside its allocation");
 
+  // memory HIP reports no range for (hipHostRegister'd pinned memory, VMM / expandable segments): the type
+  // and device checks still apply, only the extent check is skipped
+  float* vmm0 = (float*)aligned_alloc(256, K * ld * 4);
+  mockhip::add(vmm0, K * ld * 4, hipMemoryTypeDevice, 0, /*ranged=*/false);
+  float* vmm1 = (float*)aligned_alloc(256, K * ld * 4);
+  mockhip::add(vmm1, K * ld * 4, hipMemoryTypeDevice, 1, /*ranged=*/false);
+  float* reg = (float*)aligned_alloc(256, K * ld * 4);
+  mockhip::add(reg, K * ld * 4, hipMemoryTypeHost, 0, /*ranged=*/false);
+  const int l0 = launched;
+  rc = entry_reduce(vmm0, K, ld, P, a0, out0, s0);
+  expect(rc == FA_OK && launched == l0 + 1, "device memory without a HIP range (VMM segment): accepted");
+  rc = entry_reduce(vmm1, K, ld, P, a0, out0, s0);
+  expect(rc == FA_E_ARG && has("x is memory of device 1"), "rangeless memory of another device: still FA_E_ARG");
+  rc = entry_reduce(reg, K, ld, P, a0, out0, s0);
+  expect(rc == FA_OK && launched == l0 + 2, "registered pinned memory without a range where host memory is allowed");
+  rc = entry_reduce(x0, K, ld, P, (const float*)reg, out0, s0);
+  expect(rc == FA_E_ARG && has("a is pinned host memory"), "rangeless pinned memory where device memory is required");
+
   // pointer tables: 96 tensors in 3 segments of device 1 -> 3 queries per table, not 96
   const int T = 96;
   float* seg[3] = {dev_alloc(1, 1 << 20), dev_alloc(1, 1 << 20), dev_alloc(1, 1 << 20)};
@@ -124,7 +142,7 @@ int main() {
   numel[5] = 0;
   long q0 = mockhip::queries;
   rc = entry_table(param.data(), glob.data(), numel.data(), T, s1);
-  expect(rc == FA_OK && launched == 6, "table of device-1 tensors");
+  expect(rc == FA_OK && launched == l0 + 3, "table of device-1 tensors");
   printf("queries for %d + %d table pointers: %ld\n", T, T, mockhip::queries - q0);
   expect(mockhip::queries - q0 <= 6, "one query per allocation, not per tensor");
   param[40] = dev_alloc(0, 4096);

@@ -37,6 +37,7 @@ struct Alloc {
   size_t size;
   hipMemoryType type;
   int device;
+  bool ranged = true;  // false: hipMemGetAddressRange knows nothing of it (hipHostRegister'd memory, VMM segments)
 };
 inline std::map<uintptr_t, Alloc>& allocs() {
   static std::map<uintptr_t, Alloc> m;
@@ -52,8 +53,8 @@ inline int& ndev() {
 }
 inline thread_local int current = 0;
 inline long queries = 0;  // hipPointerGetAttributes calls
-inline void add(const void* base, size_t size, hipMemoryType type, int device) {
-  allocs()[(uintptr_t)base] = Alloc{(uintptr_t)base, size, type, device};
+inline void add(const void* base, size_t size, hipMemoryType type, int device, bool ranged = true) {
+  allocs()[(uintptr_t)base] = Alloc{(uintptr_t)base, size, type, device, ranged};
 }
 inline hipStream_t new_stream(int device) {
   static uintptr_t next = 0x1000;
@@ -106,7 +107,7 @@ inline hipError_t hipPointerGetAttributes(hipPointerAttribute_t* at, const void*
 }
 inline hipError_t hipMemGetAddressRange(hipDeviceptr_t* base, size_t* size, hipDeviceptr_t p) {
   const mockhip::Alloc* a = mockhip::find(p);
-  if (!a) return hipErrorInvalidValue;
+  if (!a || !a->ranged) return hipErrorInvalidValue;
   *base = (void*)a->base;
   *size = a->size;
   return hipSuccess;

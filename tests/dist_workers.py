@@ -36,7 +36,13 @@ def cpu_shard_worker(rank, world, port, name):
         g = ShardGroup(rank, world)
         shard_mean = fedavg_flat(xs[:, :lay.ld]) if K > 0 else None
         gathered = g.all_gather(torch.from_numpy(shard_mean)).numpy()
-        np.testing.assert_array_equal(gathered[:full.P_full], fedavg_flat(xf)[:full.P_full])
+        np.testing.assert_array_equal(lay.unshard(gathered), fedavg_flat(xf)[:full.P_full])
+        # the slices tile [0, P) in rank order, 64-aligned, each within 64 floats of P/world, every row ld wide
+        sizes = g.collective_all_gather(torch.tensor([lay.p0, lay.p1, lay.ld])).numpy().reshape(world, 3)
+        assert sizes[0, 0] == 0 and sizes[-1, 1] == full.P_full and (sizes[1:, 0] == sizes[:-1, 1]).all()
+        assert (sizes[:, 0] % 64 == 0).all() and (sizes[:, 2] == lay.ld).all()
+        if full.P_full >= 64 * world:
+            assert (np.abs((sizes[:, 1] - sizes[:, 0]) - full.P_full / world) <= 64).all()
         # q-FedAvg partial norms
         L = xf[0] * np.float32(0.5)
         Ls = L[lay.p0:lay.p0 + lay.ld] if lay.P else np.zeros(lay.ld, np.float32)

@@ -53,3 +53,61 @@ def test_cpu_baseline_c1_times_arithmetic_and_reference_loop():
     r = bench.cpu_baseline_c1(seed=0, rounds=3)
     assert r["kind"] == "port" and r["cores"] == 1
     assert 0 < r["round_ms"] < r["handler_round_ms"]  # the whole loop costs more than its arithmetic
+
+
+def test_pmc_traffic_belongs_to_its_run(tmp_path):
+    """roofline.traffic is looked up by (workload, resident clients, launches per round, build id): any mismatch
+    gives None (a stale entry must never be attached to a changed kernel or shape)."""
+    import json
+
+    f = tmp_path / "pmc.json"
+    key = "fedavg_k1000_p25000000_per_gpu|C1000|L4|0123456789abcdef"
+    f.write_text(json.dumps({"entries": {key: {"hbm_bytes_per_launch": 25.0e9}},
+                             "history_pre_r05": {"fedavg_k1000_p25000000": {"hbm_bytes_per_launch": 1.0}}}))
+    w = "fedavg_k1000_p25000000_per_gpu"
+    assert bench.pmc_traffic(w, 1000, 4, "0123456789abcdef", str(f)) == 25.0e9
+    assert bench.pmc_traffic(w, 1000, 4, "fedcba9876543210", str(f)) is None  # another library
+    assert bench.pmc_traffic(w, 2048, 4, "0123456789abcdef", str(f)) is None  # another chunking
+    assert bench.pmc_traffic(w, 1000, 2, "0123456789abcdef", str(f)) is None  # another launch plan
+    assert bench.pmc_traffic("fedavg_k1000_p25000000", 1000, 4, "0123456789abcdef", str(f)) is None
+    assert bench.pmc_traffic(w, 1000, 4, "0123456789abcdef", str(tmp_path / "missing.json")) is None
+
+
+def test_committed_profiles_carry_their_own_traffic():
+    """Every committed *_under_rocprof.json either has traffic null or names the PMC CSVs it came from, and its
+    traffic is within 0.1 % of what those CSVs give (tools/pmc_parse.py's correction)."""
+    import glob
+    import json
+
+    sys.path.insert(0, os.path.join(bench.ROOT, "tools"))
+    import pmc_parse
+
+    n = 0
+    for p in glob.glob(os.path.join(bench.ROOT, "profiles", "*under_rocprof*.json")):
+        line = json.loads([ln for ln in open(p).read().splitlines() if ln.startswith("{")][-1])
+        r = line["roofline"]
+        if r.get("traffic") is None:
+            continue
+        src = r["traffic_source"]
+        hbm = pmc_parse.traffic_per_launch(os.path.join(bench.ROOT, src["fetch"]), os.path.join(bench.ROOT, src["write"]),
+                                           src["kernel"], int(r["launches_per_step"]))[0]
+        assert abs(hbm / r["traffic"] - 1) < 1e-3, p
+        n += 1
+    assert n >= 6
+
+
+def test_promote_inproc_value():
+    """N > 1: value = the in-process drop-in's round; the SPMD figure stays as value_spmd; a failed in-process run
+    leaves the SPMD value and says why."""
+    res = {"value": 500000.0, "ms_per_step": 2.0, "scaling_vs_one_gpu": 7.0, "config": {"parallelism": "x"}}
+    inproc = {"ok": True, "policies": {"fedavg": {"ok": True, "inproc_round_ms": 2.5, "speedup_vs_one_gpu": 5.6,
+                                                  "devices": [0, 1, 2, 3, 4, 5, 6, 7], "transport": "rccl",
+                                                  "rounds": 20}}}
+    bench.promote_inproc(res, inproc, 1000, 20)
+    assert res["value"] == 1000 / 2.5e-3 and res["ms_per_step"] == 2.5
+    assert res["value_spmd"] == 500000.0 and res["ms_per_step_spmd"] == 2.0
+    assert res["scaling_vs_one_gpu"] == 5.6 and res["scaling_vs_one_gpu_spmd"] == 7.0
+    assert "ONE aggregator process" in res["config"]["parallelism"]
+    res2 = {"value": 1.0, "ms_per_step": 2.0, "config": {"parallelism": "x"}}
+    bench.promote_inproc(res2, {"ok": False, "policies": {"fedavg": {"ok": False, "error": "boom"}}}, 1000, 20)
+    assert res2["value"] == 1.0 and "boom" in res2["value_source"] and "value_spmd" not in res2

@@ -42,3 +42,15 @@ def test_gpu_sharded_device_path_world2(gpu_device, name):
 @pytest.mark.parametrize("name", [n for n in scenario_names() if n != "kat_linear_225"])
 def test_gpu_client_sharded_device_path_world2(gpu_device, name):
     mp.spawn(dist_workers.gpu_shard_worker, args=(2, _port(), name, 2, "clients"), nprocs=2, join=True)
+
+
+@pytest.mark.parametrize("name", ["fedavg_wide_k64", "fedavg_femnist_cnn_k10"])
+def test_cpu_sharded_reduction_world8(name):
+    """Eight ranks (BASELINE config 5's 8-way split): balanced 64-aligned slices, the all-gather reassembles the
+    unsharded mean bit for bit, and the fixed-order norm exchange matches on every rank."""
+    mp.spawn(dist_workers.cpu_shard_worker, args=(8, _port(), name), nprocs=8, join=True)
+
+
+@pytest.mark.parametrize("name", ["fedavg_wide_k64", "fedavg_femnist_cnn_k10"])
+def test_cpu_client_sharded_reduction_world8(name):
+    mp.spawn(dist_workers.cpu_client_shard_worker, args=(8, _port(), name), nprocs=8, join=True)

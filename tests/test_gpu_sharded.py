@@ -712,6 +712,48 @@ def test_registered_payload_ingress_is_bit_exact(gpu_device, parts):
         # ... loaded into the model (load_state_dict's copy_: float64 -> int64 truncates)
         loaded = [torch.as_tensor(np.asarray(w)).to(d).numpy() for w, d in zip(want, dtypes)]
         assert_state_equal(sharded.get_weights(), loaded, f"round {r} model")
-    assert sharded.registered_uploads == 2 * sum(1 for k in range(K) if k % 3 != 2)
+    # every payload upload registered, except any whose pages a neighbour's registration already covered
+    assert sharded.registered_uploads + sharded.registration_fallbacks == 2 * sum(1 for k in range(K) if k % 3 != 2)
+    assert sharded.registered_uploads >= sharded.registration_fallbacks
     sharded.close()
     assert not sharded._regs
+
+
+@pytest.mark.parametrize("kind", ["bytearray", "writable_memoryview", "readonly_bytes_view"])
+def test_mutable_payload_buffers_are_copied_before_add_returns(gpu_device, kind):
+    """the copy engine reads a registered payload AFTER on_result returns, so only an immutable root
+    (bytes, or a read-only memoryview of bytes) may be registered.  Uploads whose arrays view a bytearray or a
+    writable memoryview take the pinned-row gather (copied before add returns): overwriting the caller's buffer
+    right after on_result must not change the mean."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.sharded_model_adapter import ShardedModelAdapter
+    from oracle.cpu_reference import fedavg_close, fedavg_step
+
+    names, shapes = ["big0", "big1"], [(600_000,), (700_000,)]
+    init = [torch.zeros(s_) for s_ in shapes]
+    sharded = ShardedModelAdapter(StateDictModule(names, init), devices=[0, 0], transport="copy",
+                                  staging_capacity=8)
+    agg = DeviceAggregator(sharded)
+    rng = np.random.default_rng(11)
+    K = 6
+    agg.start_round(K)
+    acc = None
+    for k in range(K):
+        vals = [rng.standard_normal(s_[0], dtype=np.float32) for s_ in shapes]
+        acc = fedavg_step(acc, {n: v.copy() for n, v in zip(names, vals)}, k == 0)
+        raw = b"".join(v.tobytes() for v in vals)
+        root = {"bytearray": lambda: bytearray(raw), "writable_memoryview": lambda: memoryview(bytearray(raw)),
+                "readonly_bytes_view": lambda: memoryview(bytes(raw))}[kind]()
+        a0 = np.frombuffer(root, dtype=np.float32, count=shapes[0][0])
+        a1 = np.frombuffer(root, dtype=np.float32, count=shapes[1][0], offset=4 * shapes[0][0])
+        agg.on_result({"client_id": k, "update_weight": {"big0": a0, "big1": a1}, "moving_loss": 1.0})
+        if kind != "readonly_bytes_view":  # the caller reuses its receive buffer at once
+            mv = memoryview(root).cast("B")
+            mv[:] = b"\xff" * len(mv)  # NaN bit patterns everywhere
+    want = fedavg_close(acc, K)
+    assert_state_equal(sharded.get_weights(), [np.asarray(w) for w in want], kind)
+    if kind == "readonly_bytes_view":
+        assert sharded.registered_uploads + sharded.registration_fallbacks == K
+    else:
+        assert sharded.registered_uploads == 0
+    sharded.close()

@@ -1,5 +1,5 @@
 """Property tests (hypothesis) of the bucket layout: for any state_dict shape list and any world size,
-the shards tile the fp32 vector exactly, are equal-size and 64-aligned, and pack -> gather -> unpack is
+the shards tile the fp32 vector exactly, are balanced (within 64 floats) and 64-aligned, and pack -> gather -> unpack is
 the identity (the host half of the sharded path; CPU only)."""
 import numpy as np
 import torch
@@ -35,10 +35,37 @@ def test_shards_tile_and_roundtrip(entries, world, seed):
         side = i if side is None else side
         np.testing.assert_array_equal(side, i)  # the side table is replicated
     assert sum(BucketLayout(names, shapes, dtypes, r, world).P for r in range(world)) == full.P_full
-    flat = np.concatenate(parts)
-    out = full.unpack(torch.from_numpy(flat), torch.from_numpy(side))
+    flat = BucketLayout(names, shapes, dtypes, 0, world).unshard(np.concatenate(parts))  # the all-gather's rows
+    out = full.unpack(torch.from_numpy(np.ascontiguousarray(flat)), torch.from_numpy(side))
     for o, v in zip(out, vals):
         np.testing.assert_array_equal(o.numpy(), v)
+
+
+@settings(max_examples=500, deadline=None)
+@given(st.integers(0, 10**9), st.integers(1, 16))
+def test_shard_bounds_balanced_and_aligned(P, world):
+    """Parameter slices (bucket.shard_bounds): they tile [0, P) in rank order, every boundary is a multiple of 64,
+    every slice holds P/world floats within 64 (when P >= 64*world), and the common row stride ld holds each."""
+    from fedscale_amd.bucket import shard_bounds, shard_ld
+
+    b = shard_bounds(P, world)
+    assert b[0] == 0 and b[-1] == P and all(b[r] <= b[r + 1] for r in range(world))
+    assert all(x % ALIGN == 0 or x == P for x in b[:-1])  # (slices past the end are empty)
+    sizes = [b[r + 1] - b[r] for r in range(world)]
+    if P >= 64 * world:
+        assert max(abs(s_ - P / world) for s_ in sizes) <= 64
+    ld = shard_ld(P, world)
+    assert ld % ALIGN == 0 and max(sizes) <= ld < max(sizes) + ALIGN + (ALIGN if max(sizes) == 0 else 0)
+
+
+def test_eight_way_split_of_config5():
+    """BASELINE config 5's 100 M parameters over 8 GPUs: 64-aligned slices within 64 floats of 12.5 M."""
+    from fedscale_amd.bucket import shard_bounds, shard_ld
+
+    b = shard_bounds(100_000_000, 8)
+    sizes = [b[r + 1] - b[r] for r in range(8)]
+    assert sizes == [12_499_968, 12_500_032] * 4 and shard_ld(100_000_000, 8) == 12_500_032
+    assert all(x % 64 == 0 for x in b[:-1]) and max(sizes) - min(sizes) == 64
 
 
 @settings(max_examples=200, deadline=None)
@@ -67,7 +94,7 @@ def test_piece_segments_cover_every_slice_exactly():
     import numpy as np
     import torch
 
-    from fedscale_amd.bucket import BucketLayout, PieceSegments
+    from fedscale_amd.bucket import BucketLayout, PieceSegments, shard_bounds
 
     rng = np.random.default_rng(3)
     for trial in range(20):
@@ -85,9 +112,9 @@ def test_piece_segments_cover_every_slice_exactly():
         assert [segs.segs[i][1] for i in range(len(segs.segs)) if segs.segs[i][2] >= 0] == [e.numel for e in large]
         assert len(segs.large_pieces) + len(segs.small_pieces) == sum(1 for e in L.f_entries if e.numel)
         for N in (1, 2, 3, 8):
-            S = (-(-max(1, L.P_full) // N) + 63) // 64 * 64  # BucketLayout's shard
+            bnd = shard_bounds(L.P_full, N)  # BucketLayout's slices
             for r in range(N):
-                p0, p1 = min(L.P_full, r * S), min(L.P_full, (r + 1) * S)
+                p0, p1 = bnd[r], bnd[r + 1]
                 dst, nb, kind, soff = segs.part_plan(p0, p1)
                 got = sum(int(b) for b in nb)
                 assert got == 4 * (p1 - p0)
