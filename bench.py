@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--no-reassemble", action="store_true", help="skip the egress all-gather timing at N>1")
     ap.add_argument("--rest", type=float, default=None,
                     help="seconds the card idles before each heavy timed region (default %g; 0 = off)" % REST_S)
+    ap.add_argument("--mean-chain", default="auto", choices=["auto", "on", "off"],
+                    help="q-FedAvg: carry the FedAvg chain in phase 1 (auto: as the drop-in, when the round spans "
+                         "several resident chunks)")
     ap.add_argument("--sustain", type=float, default=10.0,
                     help="N = 1: seconds of back-to-back headline rounds after the rested timed region (the sustained "
                          "rate and the card's state; 0 = skip)")
@@ -790,13 +793,28 @@ def promote_inproc(res: dict, inproc: dict, K: int, steps: int) -> None:
         res["value_source"] = "spmd (the in-process drop-in run failed: %s)" % ((fa or inproc).get("error"),)
         return
     res["value_spmd"], res["ms_per_step_spmd"] = res["value"], res["ms_per_step"]
-    if "scaling_vs_one_gpu" in res:
-        res["scaling_vs_one_gpu_spmd"] = res.pop("scaling_vs_one_gpu")
+    for k in ("scaling_vs_one_gpu", "scaling_vs_one_gpu_incl_reassembly", "value_incl_reassembly",
+              "round_ms_incl_reassembly"):
+        if k in res:
+            res[k + "_spmd"] = res.pop(k)
+    if fa.get("part_kernel_ms") and fa.get("part_alg_bytes"):
+        # the per-GPU roofline of the promoted round: every part's bytes over its own kernel time, the slowest part
+        rates = [b / (ms * 1e-3) / 1e9 for b, ms in zip(fa["part_alg_bytes"], fa["part_kernel_ms"])]
+        i = min(range(len(rates)), key=rates.__getitem__)
+        L = fa.get("part_launches", [1] * len(rates))[i]
+        res["roofline_spmd"] = res["roofline"]
+        res["roofline"] = dict(res["roofline"], achieved=rates[i], frac=rates[i] / HBM_PEAK_GBS,
+                               alg_bytes_per_launch=fa["part_alg_bytes"][i] / L, launches_per_step=L,
+                               kernel_ms_per_launch=fa["part_kernel_ms"][i] / L, traffic=None,
+                               source="inproc_drop_in.fedavg: the slowest part (its bytes over its own kernel events)")
+        res["hbm_gbps"], res["kernel_ms"] = rates[i], fa["part_kernel_ms"][i]
     ms = fa["inproc_round_ms"]
     res["ms_per_step"] = ms
     res["value"] = K / (ms * 1e-3)
     res["value_source"] = ("inproc_drop_in.fedavg: one process, ShardedModelAdapter over the N GPUs, %d timed rounds "
                            "after the same warmup (synchronize on every GPU both sides)" % fa.get("rounds", steps))
+    if fa.get("egress_ms") is not None:
+        res["round_ms_incl_egress"] = fa.get("inproc_round_ms_incl_egress")
     if "speedup_vs_one_gpu" in fa:
         res["scaling_vs_one_gpu"] = fa["speedup_vs_one_gpu"]
     res["config"]["parallelism"] = (f"param-shard x{len(fa['devices'])} in ONE aggregator process "
@@ -943,7 +961,7 @@ def main():
     MEM_FRACTION = args.mem_fraction
     sets = args.sets if args.sets is not None else (2 if args.config == "c2" else 1)
     w = Workload(policy, K, P, rank, world, dev, args.seed, shards, weak=weak, budget_fraction=args.mem_fraction,
-                 sets=sets)
+                 sets=sets, mean_chain={"auto": "auto", "on": True, "off": False}[args.mean_chain])
     (wall, kern_ms_max), kern_ms, kern_ms_ranks = time_workload(w, args.steps, args.warmup, dev, world,
                                                                  args.dist_backend)
     pg_world = dist.get_world_size() if world > 1 else 1

@@ -146,8 +146,14 @@ def run(devices, K: int = 1000, P: int = 25_000_000, rounds: int = 6, warmup: in
             with p.dstream:  # the part's own device and stream
                 synth.fill(r.staging.x, K, p.layout.P, seed=seed + 7919 * i)
         r = _time_rounds(ad, [p.dstream for p in ad.parts], K, rounds, warmup)
+        from . import kernels as kx
+
         out.update({"inproc_round_ms": r["round_ms"], "part_kernel_ms": r["part_kernel_ms"], "rounds": rounds,
                     "warmup": warmup, "params_per_part": [p.layout.P for p in ad.parts],
+                    "part_launches": [kx.reduce_launches(K, p.layout.P) + (1 if policy != "fedavg" else 0)
+                                      for p in ad.parts],
+                    "part_alg_bytes": [4 * K * p.layout.P + (4 if policy == "fedavg" else 24) * p.layout.P
+                                       for p in ad.parts],
                     "client_updates_per_s": K / (r["round_ms"] * 1e-3),
                     "hbm_gbps_aggregate": alg / (r["round_ms"] * 1e-3) / 1e9,
                     "egress_ms": r["egress_ms"], "inproc_round_ms_incl_egress": r["round_ms_incl_egress"]})

@@ -99,15 +99,19 @@ def test_committed_profiles_carry_their_own_traffic():
 def test_promote_inproc_value():
     """N > 1: value = the in-process drop-in's round; the SPMD figure stays as value_spmd; a failed in-process run
     leaves the SPMD value and says why."""
-    res = {"value": 500000.0, "ms_per_step": 2.0, "scaling_vs_one_gpu": 7.0, "config": {"parallelism": "x"}}
+    res = {"value": 500000.0, "ms_per_step": 2.0, "scaling_vs_one_gpu": 7.0, "config": {"parallelism": "x"},
+           "roofline": {"achieved": 7000.0, "frac": 0.875}, "hbm_gbps": 7000.0, "kernel_ms": 1.8}
     inproc = {"ok": True, "policies": {"fedavg": {"ok": True, "inproc_round_ms": 2.5, "speedup_vs_one_gpu": 5.6,
                                                   "devices": [0, 1, 2, 3, 4, 5, 6, 7], "transport": "rccl",
-                                                  "rounds": 20}}}
+                                                  "rounds": 20, "part_kernel_ms": [1.8] * 7 + [2.0],
+                                                  "part_alg_bytes": [12.5e9] * 8, "part_launches": [1] * 8}}}
     bench.promote_inproc(res, inproc, 1000, 20)
     assert res["value"] == 1000 / 2.5e-3 and res["ms_per_step"] == 2.5
     assert res["value_spmd"] == 500000.0 and res["ms_per_step_spmd"] == 2.0
     assert res["scaling_vs_one_gpu"] == 5.6 and res["scaling_vs_one_gpu_spmd"] == 7.0
     assert "ONE aggregator process" in res["config"]["parallelism"]
+    assert res["roofline"]["achieved"] == 12.5e9 / 2.0e-3 / 1e9 and res["roofline_spmd"]["achieved"] == 7000.0
+    assert res["kernel_ms"] == 2.0 and res["roofline"]["traffic"] is None
     res2 = {"value": 1.0, "ms_per_step": 2.0, "config": {"parallelism": "x"}}
     bench.promote_inproc(res2, {"ok": False, "policies": {"fedavg": {"ok": False, "error": "boom"}}}, 1000, 20)
     assert res2["value"] == 1.0 and "boom" in res2["value_source"] and "value_spmd" not in res2
