@@ -765,17 +765,39 @@ extern "C" int fa_reduce_yogi(const float* x, int64_t ld, int32_t K, int64_t P, 
 // ------------------------------------------------------------------------------------------------
 // FedYoGi step alone (elementwise, grid-stride float4)
 // ------------------------------------------------------------------------------------------------
+// k_yogi_step touches every byte once per round.  NT: non-temporal loads and stores.  Measured back to back on
+// rotating buffer sets (tools/yogi_step_probe.py, profiles/r05_yogi_step_probe.log): 25 M 0.133 -> 0.120 ms (5.27 ->
+// 5.84 TB/s), 6.25 M 0.0314 -> 0.0299 ms, but 3.125 M 0.0148 -> 0.0164 ms: a step whose 28 P bytes fit in the
+// 256 MiB Infinity Cache keeps hits the nt policy gives up (m, v and last of the previous round, the mean just
+// written), so only steps of more than FA_YOGI_NT_MIN_BYTES take it.  Two float4 per thread per iteration: no
+// faster (same log).
+#ifndef FA_YOGI_NT_MIN_BYTES
+#define FA_YOGI_NT_MIN_BYTES (256LL << 20)
+#endif
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_y(const T* p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void st_y(T* p, T v) {
+  if (NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+template <bool NT>
 __global__ __launch_bounds__(256) void k_yogi_step(const f4* __restrict__ cur, const f4* __restrict__ last,
                                                    f4* m, f4* v, f4* out, int64_t P4, float eta, float tau,
                                                    float beta, float omb, float omb2, int init) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < P4; i += (int64_t)gridDim.x * 256) {
-    const f4 C = cur[i], L = last[i];
-    f4 M = init ? f4{0.f, 0.f, 0.f, 0.f} : m[i];
-    f4 Vv = init ? f4{tau, tau, tau, tau} : v[i];
+    const f4 C = ld_y<NT>(cur + i), L = ld_y<NT>(last + i);
+    f4 M = init ? f4{0.f, 0.f, 0.f, 0.f} : ld_y<NT>(m + i);
+    f4 Vv = init ? f4{tau, tau, tau, tau} : ld_y<NT>(v + i);
     const f4 o = yogi4(C, L, M, Vv, eta, tau, beta, omb, omb2);
-    m[i] = M;
-    v[i] = Vv;
-    out[i] = o;
+    st_y<NT>(m + i, M);
+    st_y<NT>(v + i, Vv);
+    st_y<NT>(out + i, o);
   }
 }
 
@@ -800,7 +822,8 @@ extern "C" int fa_yogi_step(const float* cur, const float* last, float* m, float
   FA_OPERAND("v", v, cols_bytes(P));
   FA_OPERAND("out", out, cols_bytes(P));
   const int64_t P4 = (P + 3) / 4;
-  hipLaunchKernelGGL(k_yogi_step, dim3(stride_grid(P4)), dim3(256), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(P4 * 16 * 7 > FA_YOGI_NT_MIN_BYTES ? k_yogi_step<true> : k_yogi_step<false>,
+                     dim3(stride_grid(P4)), dim3(256), 0, (hipStream_t)stream,
                      (const f4*)cur, (const f4*)last, (f4*)m, (f4*)v, (f4*)out, P4, eta, tau, beta, omb, omb2,
                      (flags & FA_YOGI_INIT) ? 1 : 0);
   return check_launch("fa_yogi_step");
@@ -837,7 +860,8 @@ extern "C" int fa_yogi_step_parts(int32_t n, const float* const* cur, const floa
     snprintf(what, sizeof(what), "fa_yogi_step_parts[%d]", i);
     FA_DEVICE_SCOPE(what, streams[i], out[i]);
     const int64_t P4 = (P[i] + 3) / 4;
-    hipLaunchKernelGGL(k_yogi_step, dim3(stride_grid(P4)), dim3(256), 0, (hipStream_t)streams[i], (const f4*)cur[i],
+    hipLaunchKernelGGL(P4 * 16 * 7 > FA_YOGI_NT_MIN_BYTES ? k_yogi_step<true> : k_yogi_step<false>,
+                       dim3(stride_grid(P4)), dim3(256), 0, (hipStream_t)streams[i], (const f4*)cur[i],
                        (const f4*)last[i], (f4*)m[i], (f4*)v[i], (f4*)out[i], P4, eta, tau, beta, omb, omb2,
                        (flags & FA_YOGI_INIT) ? 1 : 0);
     const int e = check_launch(what);

@@ -8,5 +8,5 @@ mkdir -p $ROOT/fedscale_amd/ab
 cd $ROOT
 while [ $# -ge 2 ]; do
   name=$1; defs=$2; shift 2
-  python3 -m fedscale_amd.buildinfo --out $ROOT/fedscale_amd/ab/libfedagg_$name.so --defs "$defs" --force
+  python3 -m fedscale_amd.buildinfo --out $ROOT/fedscale_amd/ab/libfedagg_$name.so --defs="$defs" --force
 done
