@@ -411,7 +411,7 @@ class Workload:
     device path's chunk folding does."""
 
     def __init__(self, policy, K, P_total, rank, world, dev, seed, shards, *, weak=False, chunk=None,
-                 budget_fraction=0.6, sets=1, mean_chain="auto"):
+                 budget_fraction=0.6, sets=1, mean_chain="auto", share_inputs=None):
         """``mean_chain`` (q-FedAvg): carry the plain FedAvg chain in the phase-1 kernel (fa_qfed_accumulate's
         ``chain``, the reference's model_weights, aggregator.py:497-507).  "auto" does what the drop-in does:
         fuse it whenever the round spans several resident chunks (DeviceRound, device_keep_mean=True)."""
@@ -432,15 +432,23 @@ class Workload:
             self.P, self.P_total = b[rank + 1] - b[rank], P_total
             ld = shard_ld(P_total, world)
         self.ld = ld
-        free, _ = torch.cuda.mem_get_info(dev)
-        cap = max(1, int(free * budget_fraction) // (4 * ld * sets))
-        if policy == "qfedavg":
-            cap = min(cap, kx.qfed_max_chunk())
+        if share_inputs is not None:  # the resident uploads of another workload of the same shape (paired timing)
+            cap = share_inputs.C
+        else:
+            free, _ = torch.cuda.mem_get_info(dev)
+            cap = max(1, int(free * budget_fraction) // (4 * ld * sets))
+            if policy == "qfedavg":
+                cap = min(cap, kx.qfed_max_chunk())
         self.C = min(K, cap, chunk or K)
         self.passes = [(k0, min(self.C, K - k0)) for k0 in range(0, K, self.C)]
         self.mean_chain = (len(self.passes) > 1) if mean_chain == "auto" else bool(mean_chain)
         self.xs = []
         for i in range(sets):  # sets > 1: rotate input sets so the 256 MiB Infinity Cache cannot serve repeats
+            if share_inputs is not None:
+                if share_inputs.xs[i].shape != (self.C, ld):
+                    raise ValueError("share_inputs: another shape")
+                self.xs.append(share_inputs.xs[i])
+                continue
             x = torch.empty(self.C, ld, dtype=torch.float32, device=dev)
             synth.fill(x, self.C, self.P, seed=seed + 7919 * rank + 31 * i)
             self.xs.append(x)
@@ -660,6 +668,27 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend):
 MEM_FRACTION = 0.6
 
 
+def time_paired(wa: "Workload", wb: "Workload", steps: int, dev, world, backend):
+    """Rounds of ``wa`` and ``wb`` alternating in one region (after one rest and one warmup round each); (mean ms of
+    wa's rounds, mean ms of wb's rounds), each from its own HIP event pairs on the launch stream, max over ranks."""
+    import numpy as np
+    import torch
+
+    _rest(wa, steps, dev)
+    wa.step()
+    wb.step()
+    ea = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    eb = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    _sync_all(dev, world)
+    for i in range(steps):
+        wa.step(ea[i])
+        wb.step(eb[i])
+    _sync_all(dev, world)
+    a = float(np.mean([e[0].elapsed_time(e[1]) for e in ea]))
+    b = float(np.mean([e[0].elapsed_time(e[1]) for e in eb]))
+    return _max_over_ranks([a, b], dev, world, backend)
+
+
 def config_line(name, cfg, dev, rank, world, shards, seed, backend, steps=5, warmup=2, **kw) -> dict:
     """A BASELINE config on all ranks (parameter-sharded over them), for other_configs."""
     kw.setdefault("budget_fraction", MEM_FRACTION)
@@ -691,15 +720,25 @@ def config_line(name, cfg, dev, rank, world, shards, seed, backend, steps=5, war
             out["mean_chain_note"] = ("timed as the drop-in runs this round: it spans several chunks, so the FedAvg "
                                       "chain (the reference's model_weights) is fused into phase 1; the chain-free "
                                       "kernel is beside it (no_chain)")
-            w.free()
+            # the chain-free kernel over the SAME resident uploads, its rounds alternating with the chain form's
+            # in one region (one event pair per round): the card's drift over a region hits both alike, so the
+            # pair gives the chain's cost where two separately timed regions differed by up to +-2 % (round 5)
             kw2 = dict(kw, mean_chain=False)
-            w2 = Workload(cfg["policy"], cfg["clients"], cfg["params"], rank, world, dev, seed, shards, **kw2)
-            (wall2, kern2), _, _ = time_workload(w2, steps, warmup, dev, world, backend)
-            ms2 = wall2 * 1e3 / steps
-            out["no_chain"] = {"round_ms": ms2, "dominant_kernel_ms": kern2,
-                               "hbm_gbps_kernel": w2.alg_bytes / (kern2 * 1e-3) / 1e9,
-                               "chain_cost_pct": 100.0 * (kern_max / kern2 - 1.0)}
-            w = w2
+            w2 = Workload(cfg["policy"], cfg["clients"], cfg["params"], rank, world, dev, seed, shards,
+                          share_inputs=w, **kw2)
+            pair = time_paired(w, w2, max(steps, 3), dev, world, backend)
+            out["no_chain"] = {"round_ms_paired": pair[1], "dominant_kernel_ms": pair[1],
+                               "hbm_gbps_kernel": w2.alg_bytes / (pair[1] * 1e-3) / 1e9,
+                               "chain_round_ms_paired": pair[0],
+                               "chain_cost_pct": 100.0 * (pair[0] / pair[1] - 1.0),
+                               "chain_cost_pct_unpaired_note": "the chain form's timed region above against this "
+                                                               "pair's chain-free rounds: %.2f %%" % (
+                                                                   100.0 * (kern_max / pair[1] - 1.0)),
+                               "rounds_each": max(steps, 3),
+                               "note": "rounds alternate chain / chain-free over the same resident uploads in one "
+                                       "region; one HIP event pair per round on the launch stream"}
+            w2.xs = []
+            w2.free()
     if kern_max < 1.0:  # short kernels: a HIP event pair per launch adds µs; also time back-to-back launches
         import torch
 

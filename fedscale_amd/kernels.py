@@ -180,6 +180,19 @@ def qfed_launches(ld: int, P: int, chain: bool = False) -> int:
     return int(N.load().fa_qfed_launches(int(ld), int(P), 1 if chain else 0))
 
 
+def qfed_window(chain: bool = False) -> int:
+    """Columns of one k_qfed_accum column window (one round of full-width tiles; the chain launches' tiles have their
+    own width): the largest P one launch covers, found from fa_qfed_launches."""
+    lo, hi = 1, 1 << 28  # launches(lo) == 1 < launches(hi)
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if qfed_launches((mid + 63) // 64 * 64, mid, chain) == 1:
+            lo = mid
+        else:
+            hi = mid
+    return lo
+
+
 def reduce_launches(K: int, P: int, weighted: bool = False) -> int:
     """Kernel launches one fa_reduce call makes at (K, P) on the current device (fa_reduce_launches)."""
     return int(N.load().fa_reduce_launches(int(K), int(P), 1 if weighted else 0))

@@ -136,9 +136,8 @@ def test_qfed_deferred_gathers_same_bits(gpu_device, K, P, chain):
 
     ld = round_up(P, 64)
     n = kx.qfed_launches(ld, P, chain)
-    win = 256 * 4 * (8 if chain else 16) * 256  # fedagg.hip qfed_window: one round of full-width tiles
-    nwin = -(-P // win)
-    assert nwin > 1 and n in (1, nwin)  # 1: the windows go out as one launch (QF_MULTIWIN)
+    win = kx.qfed_window(chain)  # fedagg.hip qfed_window: one round of full-width tiles
+    assert win % 4 == 0 and n == -(-P // win) and n > 1
     x = torch.empty(K, ld, device="cuda")
     synth.fill(x, K, P, seed=21)
     last = torch.empty(1, ld, device="cuda")

@@ -172,7 +172,7 @@ def test_c5_qfedavg_shard_k10000_chain_deferred_as_the_drop_in_runs_it(gpu_devic
     chunk = kx.qfed_max_chunk()
     lr, q = 0.05, 1.0
     ld = round_up(P, 64)
-    assert -(-P // (256 * 4 * 8 * 256)) > 1  # several column windows (qfed_window): the deferred gathers apply
+    assert kx.qfed_launches(ld, P, chain=True) > 1  # several column windows: the deferred gathers apply
     rng = np.random.default_rng(8)
     losses = rng.uniform(0.5, 2.0, size=K)
     alpha = np.array([np.float32(np.float_power(l + 1e-10, q)) for l in losses], dtype=np.float32)
