@@ -9,8 +9,8 @@ aggregator process (``ShardedModelAdapter``; its cross-device steps are RCCL col
 library, ``fa_rccl_*``).  ``ShardGroup`` is one process per GPU, torch.distributed over RCCL (the SPMD
 benchmark and tests), with two ways to spread a round over the ranks:
 
-* ``mode="params"`` (default): every rank owns an equal-size slice of the fp32 bucket and reduces its
-  slice of every client update.  The only collectives are the all-gather that reassembles the global model
+* ``mode="params"`` (default): every rank owns a balanced, 64-aligned slice of the fp32 bucket
+  (``bucket.shard_bounds``; every row ``ld`` wide) and reduces its slice of every client update.  The only collectives are the all-gather that reassembles the global model
   for egress and, for q-FedAvg, one exchange of the K per-client partial squared norms (all-gather +
   fixed-order sum, ``sum_partials``).  The per-element chain is the reference's, so the result is
   bit-exact.
@@ -346,12 +346,24 @@ def spmd_rccl_probe(device_index: int, group=None) -> dict:
     from . import _native
 
     rank, world = dist.get_rank(group), dist.get_world_size(group)
+    # every rank must reach ncclCommInitRank or none may (it blocks until all nranks have joined): agree first on
+    # RCCL being loadable everywhere and on rank 0's id, and skip together otherwise
+    avail = [None] * world
+    dist.all_gather_object(avail, bool(_native.load().fa_rccl_available()), group=group)
+    if not all(avail):
+        return {"skipped": "RCCL could not be loaded on ranks %s" % [r for r, a in enumerate(avail) if not a]}
     idbuf = (ctypes.c_char * 128)()
+    msg = [None]
     if rank == 0:
-        _native.call("fa_rccl_unique_id", idbuf)
-    obj = [bytes(idbuf) if rank == 0 else None]
-    dist.broadcast_object_list(obj, src=0, group=group)
-    ctypes.memmove(idbuf, obj[0], 128)
+        try:
+            _native.call("fa_rccl_unique_id", idbuf)
+            msg = [bytes(idbuf)]
+        except _native.FedAggError as e:
+            msg = [str(e)]
+    dist.broadcast_object_list(msg, src=0, group=group)
+    if not isinstance(msg[0], bytes):
+        return {"error": "fa_rccl_unique_id on rank 0: %s" % msg[0]}
+    ctypes.memmove(idbuf, msg[0], 128)
     h = ctypes.c_void_p()
     _native.call("fa_rccl_init_rank", world, idbuf, rank, device_index, ctypes.byref(h))
     try:

@@ -149,3 +149,33 @@ def gpu_shard_worker(rank, world, port, name, capacity, mode="params"):
                 assert_state_equal(got, sc.expected(r), f"{name} rank{rank} r{r}")
     finally:
         dist.destroy_process_group()
+
+
+def rccl_probe_agreement_worker(rank, world, port, unavailable_rank):
+    """spmd_rccl_probe on CPU ranks: when RCCL cannot be loaded on one rank, EVERY rank returns "skipped" together
+    (none enters the blocking ncclCommInitRank alone)."""
+    from fedscale_amd import _native
+    from fedscale_amd.state import spmd_rccl_probe
+
+    _init(rank, world, port)
+    try:
+        lib = _native.load()
+        real = lib.fa_rccl_available
+
+        class _Lib:
+            def __getattr__(self, name):
+                return getattr(lib, name)
+
+            @staticmethod
+            def fa_rccl_available():
+                return 0 if rank == unavailable_rank else real()
+
+        orig = _native.load
+        _native.load = lambda *a, **k: _Lib()
+        try:
+            r = spmd_rccl_probe(0)
+        finally:
+            _native.load = orig
+        assert "skipped" in r and str(unavailable_rank) in r["skipped"], r
+    finally:
+        dist.destroy_process_group()

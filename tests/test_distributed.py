@@ -54,3 +54,7 @@ def test_cpu_sharded_reduction_world8(name):
 @pytest.mark.parametrize("name", ["fedavg_wide_k64", "fedavg_femnist_cnn_k10"])
 def test_cpu_client_sharded_reduction_world8(name):
     mp.spawn(dist_workers.cpu_client_shard_worker, args=(8, _port(), name), nprocs=8, join=True)
+
+
+def test_rccl_probe_skips_on_every_rank_together():
+    mp.spawn(dist_workers.rccl_probe_agreement_worker, args=(3, _port(), 1), nprocs=3, join=True)
