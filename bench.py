@@ -699,7 +699,9 @@ def config_line(name, cfg, dev, rank, world, shards, seed, backend, steps=5, war
            "params_per_gpu": w.P, "resident_clients": w.C, "passes": len(w.passes), "round_ms": ms,
            "client_updates_per_s": cfg["clients"] / (ms * 1e-3),
            "hbm_gbps_per_gpu": w.alg_bytes / (ms * 1e-3) / 1e9, "dominant_kernel_ms": kern_max,
-           "hbm_gbps_kernel": w.alg_bytes / (kern_max * 1e-3) / 1e9, "card_rest_s": w.rest_s}
+           "hbm_gbps_kernel": w.alg_bytes / (kern_max * 1e-3) / 1e9, "card_rest_s": w.rest_s,
+           "card": {k: (v["mean"] if isinstance(v, dict) else v) for k, v in (getattr(w, "card", None) or {}).items()
+                    if k in ("power_w", "temp_junction_c", "temp_mem_c", "sclk_mhz", "mclk_mhz", "samples")}}
     if getattr(w, "split_ms", None):
         from fedscale_amd import kernels as kx
 
