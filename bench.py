@@ -616,12 +616,12 @@ def pmc_traffic(workload: str, resident: int, launches: int, build_id: str, path
     return None if e is None else float(e["hbm_bytes_per_launch"])
 
 
-#: seconds the card idles before each heavy timed region (--rest).  A FedScale aggregator's GPU works in bursts: one
-#: reduction per round, idle while the clients train.  After minutes of back-to-back streaming the same launches run
-#: 3-4 % slower (the card's power/thermal state, not the allocation history: tools/inline_probe.py,
-#: profiles/r04_inline_probe.log), so without a rest every config of the line would be timed in whatever state the
-#: configs before it left the card.  Outside the timed region; 0 turns it off.
-REST_S = 12.0
+#: seconds the card idles before each heavy timed region (--rest; default 0: every region is timed in the state the
+#: regions before it left the card).  Round 4 rested 12 s because one box ran the same launches 3-4 % slower after
+#: minutes of streaming (profiles/r04_inline_probe.log); round 5 measured 100 s of back-to-back headline rounds with
+#: the card's telemetry and saw no decay (profiles/r05_sustain100.json), while a rested region starts on clocks
+#: still ramping up from idle (card_state.timed_region), so the default is no rest.  Outside the timed region.
+REST_S = 0.0
 
 
 def _rest(w, steps, dev):
@@ -636,7 +636,7 @@ def _rest(w, steps, dev):
 
 def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend):
     """Warmup, then exactly ``steps`` rounds between barrier + synchronize; (wall s, mean dominant-kernel
-    ms), both max over ranks.  Heavy regions start from a rested card (``REST_S``; every rank rests alike)."""
+    ms), both max over ranks.  With ``--rest`` > 0 heavy regions start after that idle (every rank rests alike)."""
     import numpy as np
     import torch
 
