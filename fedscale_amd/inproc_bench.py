@@ -158,9 +158,13 @@ def run(devices, K: int = 1000, P: int = 25_000_000, rounds: int = 6, warmup: in
                     "hbm_gbps_aggregate": alg / (r["round_ms"] * 1e-3) / 1e9,
                     "egress_ms": r["egress_ms"], "inproc_round_ms_incl_egress": r["round_ms_incl_egress"]})
         if policy == "fedavg":
-            out["rccl"] = ad.group.rccl_info()  # what RCCL itself reports for the group's communicator
-            if ad.group.transport == "rccl":
-                out["rccl"]["all_gather_model_ms"] = _time_all_gather(ad.group, max(p.layout.ld for p in ad.parts))
+            try:  # what RCCL itself reports for the group's communicator (reported; never discards the timing)
+                out["rccl"] = ad.group.rccl_info()
+                if ad.group.transport == "rccl":
+                    out["rccl"]["all_gather_model_ms"] = _time_all_gather(ad.group,
+                                                                          max(p.layout.ld for p in ad.parts))
+            except Exception as e:
+                out["rccl"] = {"error": f"{type(e).__name__}: {e}"}
     finally:
         ad.close()
         del ad
