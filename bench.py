@@ -84,6 +84,9 @@ def parse():
     ap.add_argument("--sustain", type=float, default=10.0,
                     help="N = 1: seconds of back-to-back headline rounds after the rested timed region (the sustained "
                          "rate and the card's state; 0 = skip)")
+    ap.add_argument("--config-sustain", type=float, default=None,
+                    help="seconds of back-to-back rounds after each heavy config's rested region (default %g; 0 = off)"
+                         % 3.0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="budget of the headline CPU sample (0 = skip "
                                                                      "every CPU leg)")
     ap.add_argument("--seed", type=int, default=2024)
@@ -616,31 +619,35 @@ def pmc_traffic(workload: str, resident: int, launches: int, build_id: str, path
     return None if e is None else float(e["hbm_bytes_per_launch"])
 
 
-#: seconds the card idles before each heavy timed region (--rest; default 0: every region is timed in the state the
-#: regions before it left the card).  Round 4 rested 12 s because one box ran the same launches 3-4 % slower after
-#: minutes of streaming (profiles/r04_inline_probe.log); round 5 measured 100 s of back-to-back headline rounds with
-#: the card's telemetry and saw no decay (profiles/r05_sustain100.json), while a rested region starts on clocks
-#: still ramping up from idle (card_state.timed_region), so the default is no rest.  Outside the timed region.
-REST_S = 0.0
+#: seconds the card idles before each heavy timed region of ``other_configs`` (--rest; the headline's region, the first
+#: of the line, takes no rest unless --rest is given).  100 s of back-to-back headline rounds showed no decay
+#: (profiles/r05_sustain100.json), but the configs timed one after another do: without a rest config 5 on one GPU ran
+#: at the board's 1400 W cap (1384 W mean) with the shader clock down to 2150 MHz, and the shard of 8 timed after it at
+#: 1810 MHz, 3 % slower (profiles/r05_bench_default_n1_norest.json).  An aggregator's GPU works in bursts (one round,
+#: then idle while the clients train), so each config is timed from a rested card and ALSO back to back right after
+#: (``sustained`` on each config line), both with the card's telemetry.  Outside the timed region.
+REST_S = 12.0
+HEADLINE_REST_S = 0.0  # --rest sets both
 
 
-def _rest(w, steps, dev):
+def _rest(w, steps, dev, rest_s=None):
     import torch
 
-    if REST_S > 0 and w.alg_bytes * max(1, steps) > 20e9:  # heavy regions only (c2's 0.4 GB rounds need none)
+    REST_S_ = REST_S if rest_s is None else rest_s
+    if REST_S_ > 0 and w.alg_bytes * max(1, steps) > 20e9:  # heavy regions only (c2's 0.4 GB rounds need none)
         torch.cuda.synchronize(dev)
-        time.sleep(REST_S)
-        return REST_S
+        time.sleep(REST_S_)
+        return REST_S_
     return 0.0
 
 
-def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend):
+def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend, rest_s=None):
     """Warmup, then exactly ``steps`` rounds between barrier + synchronize; (wall s, mean dominant-kernel
     ms), both max over ranks.  With ``--rest`` > 0 heavy regions start after that idle (every rank rests alike)."""
     import numpy as np
     import torch
 
-    w.rest_s = _rest(w, steps, dev)
+    w.rest_s = _rest(w, steps, dev, rest_s)
     for _ in range(warmup):
         w.step()
     split = w.yogi is not None and not w.cmode  # FedYoGi: a third event between the mean and the YoGi step
@@ -666,6 +673,7 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend):
 
 
 MEM_FRACTION = 0.6
+CONFIG_SUSTAIN_S = 3.0  # back-to-back seconds after each heavy config's rested region (--config-sustain)
 
 
 def time_paired(wa: "Workload", wb: "Workload", steps: int, dev, world, backend):
@@ -702,6 +710,13 @@ def config_line(name, cfg, dev, rank, world, shards, seed, backend, steps=5, war
            "hbm_gbps_kernel": w.alg_bytes / (kern_max * 1e-3) / 1e9, "card_rest_s": w.rest_s,
            "card": {k: (v["mean"] if isinstance(v, dict) else v) for k, v in (getattr(w, "card", None) or {}).items()
                     if k in ("power_w", "temp_junction_c", "temp_mem_c", "sclk_mhz", "mclk_mhz", "samples")}}
+    if CONFIG_SUSTAIN_S > 0 and world == 1 and w.alg_bytes * max(1, steps) > 20e9:
+        # the same rounds back to back right after the rested region (no rest): the rate this config settles at
+        # (one GPU only: the ranks' rounds would not stay in step through a time-bounded loop's collectives)
+        sus = sustained_leg(w, dev, CONFIG_SUSTAIN_S, 1, ms, window_s=CONFIG_SUSTAIN_S, chunk_s=0.5)
+        out["sustained"] = {"round_ms": sus["ms_per_step"], "hbm_gbps_kernel": sus["hbm_gbps"],
+                            "seconds": sus["seconds"], "rounds": sus["steps"],
+                            "card": {k: v["mean"] for k, v in sus["card_window"].items() if isinstance(v, dict)}}
     if getattr(w, "split_ms", None):
         from fedscale_amd import kernels as kx
 
@@ -916,7 +931,8 @@ def one_gpu_reference(policy, K, P, dev, seed, steps=5, warmup=2) -> dict:
     return {"ms_per_step": ms, "client_updates_per_s": K / (ms * 1e-3), "steps": steps}
 
 
-def sustained_leg(w: "Workload", dev, seconds: float, launches: int, est_ms: float, window_s: float = 3.0) -> dict:
+def sustained_leg(w: "Workload", dev, seconds: float, launches: int, est_ms: float, window_s: float = 3.0,
+                  chunk_s: float = 1.0) -> dict:
     """Back-to-back rounds of the headline workload for ``seconds`` right after its rested timed region, no rest:
     the rate a card streaming without pause settles at, beside the card's power, temperatures and clocks (sysfs,
     fedscale_amd/cardstate.py).  Chunks of ~1 s, each timed by one HIP event pair on the launch stream;
@@ -926,7 +942,7 @@ def sustained_leg(w: "Workload", dev, seconds: float, launches: int, est_ms: flo
 
     from fedscale_amd.cardstate import CardSampler
 
-    per_chunk = max(1, int(round(1000.0 / max(est_ms, 1e-3))))
+    per_chunk = max(1, int(round(1000.0 * chunk_s / max(est_ms, 1e-3))))
     sampler = CardSampler(dev, period_s=0.05)
     torch.cuda.synchronize(dev)
     sampler.start()
@@ -964,8 +980,11 @@ def sustained_leg(w: "Workload", dev, seconds: float, launches: int, est_ms: flo
 def main():
     global REST_S
     args = parse()
+    global HEADLINE_REST_S, CONFIG_SUSTAIN_S
+    if args.config_sustain is not None:
+        CONFIG_SUSTAIN_S = max(0.0, args.config_sustain)
     if args.rest is not None:
-        REST_S = max(0.0, args.rest)
+        REST_S = HEADLINE_REST_S = max(0.0, args.rest)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -1004,7 +1023,7 @@ def main():
     w = Workload(policy, K, P, rank, world, dev, args.seed, shards, weak=weak, budget_fraction=args.mem_fraction,
                  sets=sets, mean_chain={"auto": "auto", "on": True, "off": False}[args.mean_chain])
     (wall, kern_ms_max), kern_ms, kern_ms_ranks = time_workload(w, args.steps, args.warmup, dev, world,
-                                                                 args.dist_backend)
+                                                                 args.dist_backend, rest_s=HEADLINE_REST_S)
     pg_world = dist.get_world_size() if world > 1 else 1
     strong = not weak and not w.cmode
     card_state = {"before_timed_region": w.card_before, "timed_region": w.card, "rest_s": w.rest_s}
@@ -1116,7 +1135,7 @@ def main():
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic full-weight client updates (base + noise, hash-generated on device), HBM-resident",
             "host_numa_node": numa_node,
-            "card_rest_s": REST_S,
+            "card_rest_s": HEADLINE_REST_S, "other_configs_card_rest_s": REST_S,
             "build_id": build_id,
             "config": config,
             "hbm_gbps": achieved,
