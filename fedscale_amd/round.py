@@ -90,11 +90,16 @@ class DeviceRound:
         K_local = max(1, self.k_end - self.k_begin)
         if policy == "qfedavg":
             qmax = kx.qfed_max_chunk()
-            capacity = min(capacity or qmax, qmax)
+            implicit = capacity is None
+            capacity = min(capacity or qmax, qmax)  # phase-1 calls take at most fa_qfed_max_chunk() clients
+        else:
+            implicit = False
         if staging is not None and (capacity is None or staging.capacity >= min(capacity, K_local)):
             self.staging = staging
         else:
             cap = capacity or default_capacity(layout, K_local, self.device)
+            if implicit:  # ... and no more than fit the free HBM (a 100 M-parameter model: ~360, not 2048)
+                cap = min(cap, default_capacity(layout, K_local, self.device))
             self.staging = ClientStaging(layout, self.device, min(cap, K_local), dstream=self.dstream)
         self.cap = min(self.staging.capacity, capacity or self.staging.capacity)
         self.staging.generation += 1  # a new round takes the staging slots over

@@ -288,3 +288,24 @@ def test_get_weights_of_a_large_model_clones_in_parallel(gpu_device):
     assert len({t.data_ptr() for t in got}) == len(got)
     got[0].fill_(7.0)
     assert_state_equal(ad.get_weights(), want, "a second call after the caller wrote into the first list")
+
+
+def test_qfed_round_without_capacity_is_sized_by_free_hbm(gpu_device, monkeypatch):
+    """A q-FedAvg DeviceRound given no capacity (TorchServerOptimizer's reference-typed list path) stages at most
+    what default_capacity admits, not fa_qfed_max_chunk() clients: 2048 rows of a 100 M-parameter model would not
+    fit the card."""
+    from fedscale_amd import round as rd
+    from fedscale_amd.bucket import BucketLayout
+
+    seen = []
+
+    def small(layout, K, device, *a, **k):
+        seen.append(K)
+        return 4
+
+    monkeypatch.setattr(rd, "default_capacity", small)
+    lay = BucketLayout(["w"], [(1000,)], [torch.float32])
+    rnd = rd.DeviceRound(lay, "cuda:0", 11, "qfedavg")
+    assert seen and rnd.staging.capacity == 4 and rnd.cap == 4
+    rnd2 = rd.DeviceRound(lay, "cuda:0", 11, "qfedavg", capacity=6)  # an explicit capacity is kept
+    assert rnd2.staging.capacity == 6 and rnd2.cap == 6
