@@ -36,6 +36,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import platform
 import sys
@@ -674,6 +675,7 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend, res
 
 MEM_FRACTION = 0.6
 CONFIG_SUSTAIN_S = 3.0  # back-to-back seconds after each heavy config's rested region (--config-sustain)
+PAIR_S = 3.0  # seconds of each form in config 5's paired chain / chain-free region
 
 
 def time_paired(wa: "Workload", wb: "Workload", steps: int, dev, world, backend):
@@ -743,7 +745,10 @@ def config_line(name, cfg, dev, rank, world, shards, seed, backend, steps=5, war
             kw2 = dict(kw, mean_chain=False)
             w2 = Workload(cfg["policy"], cfg["clients"], cfg["params"], rank, world, dev, seed, shards,
                           share_inputs=w, **kw2)
-            pair = time_paired(w, w2, max(steps, 3), dev, world, backend)
+            # about PAIR_S seconds of each form (config 5 on one GPU: 6 rounds each; its shard of 8: ~40): the
+            # chain cost is 1-2 % of a round, and 3 rounds each read 1.5-6 % on one box (profiles/r05_budget*_paired.log)
+            n_pair = max(steps, 3, int(math.ceil(PAIR_S / max(kern_max * 1e-3, 1e-6))))
+            pair = time_paired(w, w2, n_pair, dev, world, backend)
             out["no_chain"] = {"round_ms_paired": pair[1], "dominant_kernel_ms": pair[1],
                                "hbm_gbps_kernel": w2.alg_bytes / (pair[1] * 1e-3) / 1e9,
                                "chain_round_ms_paired": pair[0],
@@ -751,7 +756,7 @@ def config_line(name, cfg, dev, rank, world, shards, seed, backend, steps=5, war
                                "chain_cost_pct_unpaired_note": "the chain form's timed region above against this "
                                                                "pair's chain-free rounds: %.2f %%" % (
                                                                    100.0 * (kern_max / pair[1] - 1.0)),
-                               "rounds_each": max(steps, 3),
+                               "rounds_each": n_pair,
                                "note": "rounds alternate chain / chain-free over the same resident uploads in one "
                                        "region; one HIP event pair per round on the launch stream"}
             w2.xs = []

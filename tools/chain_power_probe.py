@@ -1,7 +1,7 @@
 """Is config 5's one-GPU chain cost a power-cap effect?  The chain form and the chain-free kernel over the same
 resident uploads (bench.Workload, share_inputs), each run back to back for its own region, alternating, with the
 card's power and shader clock sampled per region.  If the chain rounds draw more power at the 1400 W cap, their
-shader clock sits lower than the chain-free rounds'.  usage: python tools/chain_power_probe.py [P] [seconds]"""
+shader clock sits lower than the chain-free rounds'.  usage: python tools/chain_power_probe.py [P] [seconds] [HBM budget fraction for the resident uploads]"""
 import json
 import os
 import sys
@@ -37,15 +37,17 @@ def region(w, dev, seconds, tag):
 def main():
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000_000
     seconds = float(sys.argv[2]) if len(sys.argv) > 2 else 4.0
+    budget = float(sys.argv[3]) if len(sys.argv) > 3 else bench.MEM_FRACTION
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     cfg = dict(bench.CONFIGS["c5"], params=P)
     sh = ShardGroup(0, 1)
     wc = bench.Workload(cfg["policy"], cfg["clients"], cfg["params"], 0, 1, dev, 2024, sh,
-                        budget_fraction=bench.MEM_FRACTION, mean_chain=True)
+                        budget_fraction=budget, mean_chain=True)
     wf = bench.Workload(cfg["policy"], cfg["clients"], cfg["params"], 0, 1, dev, 2024, sh,
-                        budget_fraction=bench.MEM_FRACTION, mean_chain=False, share_inputs=wc)
-    print(json.dumps({"params": P, "resident_clients": wc.C, "passes": len(wc.passes)}), flush=True)
+                        budget_fraction=budget, mean_chain=False, share_inputs=wc)
+    print(json.dumps({"params": P, "budget_fraction": budget, "resident_clients": wc.C, "passes": len(wc.passes)}),
+          flush=True)
     wc.step()
     wf.step()
     out = {"chain": [], "free": []}
