@@ -305,7 +305,9 @@ def test_qfed_round_without_capacity_is_sized_by_free_hbm(gpu_device, monkeypatc
 
     monkeypatch.setattr(rd, "default_capacity", small)
     lay = BucketLayout(["w"], [(1000,)], [torch.float32])
-    rnd = rd.DeviceRound(lay, "cuda:0", 11, "qfedavg")
+    last = dict(last_f32=torch.zeros(lay.ld, dtype=torch.float32, device="cuda:0"),
+                last_i64=torch.zeros(max(1, lay.ldq), dtype=torch.int64, device="cuda:0"))
+    rnd = rd.DeviceRound(lay, "cuda:0", 11, "qfedavg", **last)
     assert seen and rnd.staging.capacity == 4 and rnd.cap == 4
-    rnd2 = rd.DeviceRound(lay, "cuda:0", 11, "qfedavg", capacity=6)  # an explicit capacity is kept
+    rnd2 = rd.DeviceRound(lay, "cuda:0", 11, "qfedavg", capacity=6, **last)  # an explicit capacity is kept
     assert rnd2.staging.capacity == 6 and rnd2.cap == 6
