@@ -65,7 +65,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=-1,
+                    help="untimed warmup rounds; -1 (default): at least 3 and, at N = 1, at least 1 s of them, so the "
+                         "timed region starts with the card's clocks settled (the line reports the count)")
     ap.add_argument("--config", default="headline", choices=sorted(CONFIGS))
     ap.add_argument("--clients", type=int, default=None, help="override the config's K")
     ap.add_argument("--params", type=int, default=None,
@@ -649,8 +651,19 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend, res
     import torch
 
     w.rest_s = _rest(w, steps, dev, rest_s)
-    for _ in range(warmup):
-        w.step()
+    if warmup < 0:  # auto: at least 3 rounds and, on one GPU, at least WARMUP_S seconds of them (clocks settled)
+        import torch
+
+        n, t0 = 0, time.perf_counter()
+        while n < 3 or (world == 1 and time.perf_counter() - t0 < WARMUP_S):
+            w.step()
+            torch.cuda.synchronize(dev)
+            n += 1
+        warmup = n
+    else:
+        for _ in range(warmup):
+            w.step()
+    w.warmup_rounds = warmup
     split = w.yogi is not None and not w.cmode  # FedYoGi: a third event between the mean and the YoGi step
     evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3 if split else 2)) for _ in range(steps)]
     from fedscale_amd.cardstate import CardSampler
@@ -676,6 +689,7 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend, res
 MEM_FRACTION = 0.6
 CONFIG_SUSTAIN_S = 3.0  # back-to-back seconds after each heavy config's rested region (--config-sustain)
 PAIR_S = 3.0  # seconds of each form in config 5's paired chain / chain-free region
+WARMUP_S = 1.0  # --warmup -1: seconds of untimed rounds before the headline's timed region (one GPU)
 
 
 def time_paired(wa: "Workload", wb: "Workload", steps: int, dev, world, backend):
@@ -1029,6 +1043,7 @@ def main():
                  sets=sets, mean_chain={"auto": "auto", "on": True, "off": False}[args.mean_chain])
     (wall, kern_ms_max), kern_ms, kern_ms_ranks = time_workload(w, args.steps, args.warmup, dev, world,
                                                                  args.dist_backend, rest_s=HEADLINE_REST_S)
+    warmup_used = w.warmup_rounds  # --warmup -1: the count the auto warmup ran
     pg_world = dist.get_world_size() if world > 1 else 1
     strong = not weak and not w.cmode
     card_state = {"before_timed_region": w.card_before, "timed_region": w.card, "rest_s": w.rest_s}
@@ -1095,7 +1110,7 @@ def main():
         if rank == 0:
             one_gpu = one_gpu_reference(policy, K, P, dev, args.seed)
             if policy == "fedavg":
-                inproc = run_inproc_bench(world, K, P, args.dist_backend, steps=args.steps, warmup=args.warmup)
+                inproc = run_inproc_bench(world, K, P, args.dist_backend, steps=args.steps, warmup=warmup_used)
         dist.barrier(group=cpu_group)
 
     selfcheck = None
@@ -1136,7 +1151,7 @@ def main():
                        if policy == "fedavg" else
                        f"client-updates/sec + HBM GB/s, device-resident {policy} round of KxP fp32"),
             "value": value, "unit": "client-updates/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True,
+            "warmup": warmup_used, "ms_per_step": ms_per_step, "higher_is_better": True,
             "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic full-weight client updates (base + noise, hash-generated on device), HBM-resident",
             "host_numa_node": numa_node,

@@ -30,7 +30,8 @@ def test_configs_are_baselines():
 def test_default_arguments(monkeypatch):
     monkeypatch.setattr(sys, "argv", ["bench.py"])
     a = bench.parse()
-    assert a.gpus == 1 and a.steps > 0 and a.warmup >= 0 and a.steps * 15e-3 < 60
+    assert a.gpus == 1 and a.steps > 0 and a.steps * 15e-3 < 60
+    assert a.warmup == -1 and bench.WARMUP_S <= 2.0  # auto: >= 3 rounds and ~1 s of them, a bounded prefix
     assert a.cfg == bench.CONFIGS["headline"] and a.scaling == "strong" and a.dist_backend == "nccl"
     monkeypatch.setattr(sys, "argv", ["bench.py", "--config", "c5", "--params", "1000"])
     a = bench.parse()
