@@ -1,0 +1,117 @@
+"""Randomised parity of the hot-path kernels through the C ABI (hypothesis drives the shapes): K, P, the row
+pitch ld, weights, chunk splits (acc_in continuation) and, for q-FedAvg, the FedAvg chain and the call's client
+count, each against the oracle's flat restatement of the reference arithmetic.
+
+* FedAvg / FedBuff (aggregator.py:497-507, async_aggregator.py:125-135): bit-exact, in one call or split into
+  two chunks that continue the chain (DeviceRound's chunk folding), from device rows or from pinned host rows.
+* q-FedAvg phase 1 (optimizers.py:82-98): the delta chain and the FedAvg chain bit-exact, the per-client squared
+  norms within 5e-7 relative: the kernel sums fp32 partials of 4 (8 in chain launches) squares in fp64 in a fixed
+  order, so a norm of a few elements carries up to 7 fp32 roundings (the reference's own torch CPU order is
+  implementation-defined); with the chain fused or not, in one call or two.
+Inputs are seeded and sized so the whole file runs in seconds; the shapes include P below one strip, P not a
+multiple of 4, ld with padding, K = 1, and column counts just past a strip or a tile."""
+import numpy as np
+import pytest
+import torch
+from hypothesis import HealthCheck, example, given, settings
+from hypothesis import strategies as st
+
+from oracle.cpu_reference import fedavg_flat, fedbuff_flat
+
+pytestmark = pytest.mark.gpu
+
+SETTINGS = settings(max_examples=100, deadline=None, derandomize=True,
+                    suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+P_EDGES = [1, 3, 4, 63, 64, 65, 255, 256, 257, 1023, 4097, 16383, 65537, 262147]
+
+
+def _rows(rng, K, P, ld, scale=0.05):
+    base = rng.normal(0, scale, size=P).astype(np.float32)
+    x = np.zeros((K, ld), dtype=np.float32)
+    x[:, :P] = base[None, :] + rng.normal(0, 0.01, size=(K, P)).astype(np.float32)
+    return x
+
+
+shapes = st.tuples(st.integers(1, 33), st.one_of(st.sampled_from(P_EDGES), st.integers(1, 70000)),
+                   st.sampled_from([0, 4, 60, 64]), st.integers(0, 2 ** 31 - 1))
+
+
+@SETTINGS
+@given(shape=shapes, weighted=st.booleans(), split=st.integers(0, 32), host=st.booleans())
+@example(shape=(33, 262147, 64, 1), weighted=True, split=17, host=False)
+@example(shape=(33, 262147, 60, 2), weighted=False, split=0, host=True)
+@example(shape=(1, 65537, 0, 3), weighted=True, split=0, host=False)
+@example(shape=(32, 70000, 4, 4), weighted=False, split=31, host=True)
+def test_reduce_matches_oracle(gpu_device, shape, weighted, split, host):
+    from fedscale_amd import kernels as kx
+
+    K, P, pad, seed = shape
+    ld = (P + 3) // 4 * 4 + pad
+    rng = np.random.default_rng(seed)
+    xh = _rows(rng, K, P, ld)
+    s = [1 / (1 + int(v)) ** 0.5 for v in rng.integers(0, 6, size=K)] if weighted else None
+    want = fedbuff_flat(xh[:, :P], s) if weighted else fedavg_flat(xh[:, :P])
+    denom = float(np.float32(sum(s))) if weighted else float(np.float32(K))
+    a = torch.tensor(np.asarray(s, dtype=np.float32), device="cuda") if weighted else None
+    if host:
+        x = torch.from_numpy(xh).pin_memory()
+    else:
+        x = torch.from_numpy(xh).cuda()
+    out = torch.full((kx._cols(P),), float("nan"), device="cuda")
+    h = split % K  # 0: one call; otherwise two chunks [0, h) and [h, K) continuing the chain
+    if h == 0:
+        kx.reduce(x, K, P, out, a=a, denom=denom, finalize=True, host_ok=host)
+    else:
+        acc = torch.empty(kx._cols(P), device="cuda")
+        kx.reduce(x[:h], h, P, acc, a=None if a is None else a[:h], host_ok=host)
+        kx.reduce(x[h:], K - h, P, out, a=None if a is None else a[h:], acc_in=acc, denom=denom, finalize=True,
+                  host_ok=host)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(out[:P].cpu().numpy(), want)
+
+
+@SETTINGS
+@given(shape=shapes, chain=st.booleans(), split=st.integers(0, 32), q=st.sampled_from([0.0, 1.0, 2.0]),
+       lr=st.sampled_from([0.05, 0.1, 1 / 3]))
+@example(shape=(33, 262147, 64, 5), chain=True, split=20, q=1.0, lr=0.05)
+@example(shape=(33, 262147, 0, 6), chain=False, split=0, q=2.0, lr=1 / 3)
+@example(shape=(5, 65537, 60, 7), chain=True, split=0, q=0.0, lr=0.1)
+@example(shape=(32, 70000, 4, 8), chain=True, split=1, q=1.0, lr=0.05)
+def test_qfed_accumulate_matches_oracle(gpu_device, shape, chain, split, q, lr):
+    from fedscale_amd import kernels as kx
+
+    K, P, pad, seed = shape
+    ld = (P + 3) // 4 * 4 + pad
+    rng = np.random.default_rng(seed)
+    xh = _rows(rng, K, P, ld)
+    L = np.zeros(ld, dtype=np.float32)
+    L[:P] = xh[:, :P].mean(axis=0, dtype=np.float32) + np.float32(0.001)
+    losses = rng.uniform(0.5, 2.0, size=K)
+    alpha = np.array([np.float32(np.float_power(v + 1e-10, q)) for v in losses], dtype=np.float32)
+    # optimizers.py:82-93 in fp32, arrival order; aggregator.py:497-503's chain of the same uploads
+    d = c = None
+    sq_ref = np.zeros(K)
+    for k in range(K):
+        g = (L[:P] - xh[k, :P]) / np.float32(lr)
+        t = alpha[k] * g
+        d = t if d is None else d + t
+        c = xh[k, :P] if c is None else c + xh[k, :P]
+        sq_ref[k] = np.sum((g * g).astype(np.float64))
+    x = torch.from_numpy(xh).cuda()
+    Ld = torch.from_numpy(L).cuda()
+    al = torch.from_numpy(alpha).cuda()
+    cols = kx._cols(P)
+    delta = torch.full((cols,), float("nan"), device="cuda")
+    ch = torch.full((cols,), float("nan"), device="cuda") if chain else None
+    sq = torch.zeros(K, dtype=torch.float64, device="cuda")  # fa_qfed_accumulate adds into sqnorm (fedagg.h)
+    ws = kx.qfed_workspace(K, "cuda", ld, P)
+    h = split % K
+    parts = [(0, K)] if h == 0 else [(0, h), (h, K)]
+    for i, (k0, k1) in enumerate(parts):
+        kx.qfed_accumulate(x[k0:k1], k1 - k0, P, last=Ld, alpha=al[k0:k1], lr=lr, delta=delta, sqnorm=sq[k0:k1],
+                           workspace=ws, accumulate=i > 0, chain=ch)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(delta[:P].cpu().numpy(), d)
+    if chain:
+        np.testing.assert_array_equal(ch[:P].cpu().numpy(), c)
+    np.testing.assert_allclose(sq.cpu().numpy(), sq_ref, rtol=5e-7, atol=0)
