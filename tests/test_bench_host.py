@@ -75,8 +75,10 @@ def test_pmc_traffic_belongs_to_its_run(tmp_path):
 
 
 def test_committed_profiles_carry_their_own_traffic():
-    """Every committed *_under_rocprof.json either has traffic null or names the PMC CSVs it came from, and its
-    traffic is within 0.1 % of what those CSVs give (tools/pmc_parse.py's correction)."""
+    """Every committed *_under_rocprof.json either has traffic null, or names the PMC CSVs it came from and its
+    traffic is within 0.1 % of what those CSVs give (tools/pmc_parse.py's correction), or (a plain bench line run
+    under the profiler) carries exactly the keyed pmc_traffic.json entry of its own workload, resident clients,
+    launches per round and build id."""
     import glob
     import json
 
@@ -88,6 +90,10 @@ def test_committed_profiles_carry_their_own_traffic():
         line = json.loads([ln for ln in open(p).read().splitlines() if ln.startswith("{")][-1])
         r = line["roofline"]
         if r.get("traffic") is None:
+            continue
+        if "traffic_source" not in r:
+            assert r["traffic"] == bench.pmc_traffic(line["config"]["workload"], r["resident_clients"],
+                                                     r["launches_per_step"], line["build_id"]), p
             continue
         src = r["traffic_source"]
         hbm = pmc_parse.traffic_per_launch(os.path.join(bench.ROOT, src["fetch"]), os.path.join(bench.ROOT, src["write"]),
