@@ -1527,6 +1527,33 @@ __global__ __launch_bounds__(256) void k_qfed_gather_win(const double* __restric
   sqnorm[k] = acc;
 }
 
+// The same sums with one wave per client: lane l forms the window sums s_w of windows w = l, l + 64, ... (each from
+// 0.0 over its 16 segments in order, as above) into LDS, then lane 0 adds them to sqnorm[k] in window order — the
+// same adds in the same order, so the same bits.  One memory round trip per 64 windows instead of one per window:
+// the thread-per-client form above waits on nwin dependent batches of loads (config 5 on one GPU: 50 windows, 57-68
+// us per call, profiles/r05_prof_all_by_shape.jsonl).
+#define QF_GWIN_MAX 1024  // windows per call this form takes (the host keeps the form above beyond it)
+__global__ __launch_bounds__(256) void k_qfed_gather_win_wave(const double* __restrict__ seg, int K, int nwin,
+                                                              double* sqnorm) {
+  __shared__ double sw[4][QF_GWIN_MAX];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int k = blockIdx.x * 4 + wave;
+  if (k < K) {
+    for (int w = lane; w < nwin; w += 64) {
+      double s = 0.0;
+#pragma unroll
+      for (int b = 0; b < QF_GATHER_SEG; ++b) s += seg[((int64_t)w * QF_GATHER_SEG + b) * K + k];
+      sw[wave][w] = s;
+    }
+  }
+  __syncthreads();
+  if (k < K && lane == 0) {
+    double acc = sqnorm[k];
+    for (int w = 0; w < nwin; ++w) acc += sw[wave][w];
+    sqnorm[k] = acc;
+  }
+}
+
 extern "C" int fa_qfed_max_chunk(void) { return QF_MAXK; }
 
 static int64_t qfed_window(int64_t ld, int64_t P, bool chain);
@@ -1562,6 +1589,9 @@ extern "C" int64_t fa_qfed_workspace_bytes(int32_t K, int64_t ld, int64_t P) {
 #endif
 #if !FA_TUNING && ((defined(QF_KERNEL) && QF_KERNEL != 1) || QF_CHAIN_KERNEL != 1)
 #error "QF_KERNEL / QF_CHAIN_KERNEL 2 (k_qfed_accum2) is a tuning build: add -DFA_TUNING=1"
+#endif
+#ifndef QF_GATHER_WAVE
+#define QF_GATHER_WAVE 1  // deferred gathers: the wave-per-client window fold (k_qfed_gather_win_wave)
 #endif
 #ifndef QF_DEFER_GATHER
 #define QF_DEFER_GATHER 1  // one gather pair per call over every window's partials (workspace permitting)
@@ -1674,8 +1704,12 @@ static int launch_qfed1(const float* x, int64_t ld, int32_t K, int64_t P, const 
     double* seg = (double*)workspace + nw * per_win;
     hipLaunchKernelGGL(k_qfed_gather_seg_win, dim3((K + 255) / 256, QF_GATHER_SEG, (unsigned)nw), dim3(256), 0, st,
                        (const double*)workspace, grid, (int)K, per_win, seg);
-    hipLaunchKernelGGL(k_qfed_gather_win, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)seg, (int)K,
-                       (int)nw, sqnorm);
+    if (QF_GATHER_WAVE && nw <= QF_GWIN_MAX)
+      hipLaunchKernelGGL(k_qfed_gather_win_wave, dim3((K + 3) / 4), dim3(256), 0, st, (const double*)seg, (int)K,
+                         (int)nw, sqnorm);
+    else
+      hipLaunchKernelGGL(k_qfed_gather_win, dim3((K + 255) / 256), dim3(256), 0, st, (const double*)seg, (int)K,
+                         (int)nw, sqnorm);
     return check_launch("fa_qfed_accumulate(gather)");
   }
   return FA_OK;
