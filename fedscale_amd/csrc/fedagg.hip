@@ -1801,13 +1801,34 @@ __global__ __launch_bounds__(256) void k_qfed_hs(const double* sqnorm, const flo
     }
     __syncthreads();
     if (threadIdx.x == 0) {
+      // the adds stay one dependent chain in k order; the LDS reads run one 32-term batch ahead of them, so the
+      // chain waits on the adds alone (a read per 4 terms in the loop's critical path cost ~34 cycles per term:
+      // 142 us at K = 10,000, profiles/r05_prof_all_by_shape.jsonl)
       int i = 0;
-      for (; i + 4 <= n; i += 4) {
-        const float4 t = *reinterpret_cast<const float4*>(terms + i);
-        hs = hs + t.x;
-        hs = hs + t.y;
-        hs = hs + t.z;
-        hs = hs + t.w;
+      if (n >= 32) {
+        float4 cur[8], nxt[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) cur[j] = *reinterpret_cast<const float4*>(terms + 4 * j);
+        for (; i + 64 <= n; i += 32) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) nxt[j] = *reinterpret_cast<const float4*>(terms + i + 32 + 4 * j);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            hs = hs + cur[j].x;
+            hs = hs + cur[j].y;
+            hs = hs + cur[j].z;
+            hs = hs + cur[j].w;
+            cur[j] = nxt[j];
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          hs = hs + cur[j].x;
+          hs = hs + cur[j].y;
+          hs = hs + cur[j].z;
+          hs = hs + cur[j].w;
+        }
+        i += 32;
       }
       for (; i < n; ++i) hs = hs + terms[i];
     }

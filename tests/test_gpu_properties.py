@@ -115,3 +115,29 @@ def test_qfed_accumulate_matches_oracle(gpu_device, shape, chain, split, q, lr):
     if chain:
         np.testing.assert_array_equal(ch[:P].cpu().numpy(), c)
     np.testing.assert_allclose(sq.cpu().numpy(), sq_ref, rtol=5e-7, atol=0)
+
+
+@settings(max_examples=60, deadline=None, derandomize=True,
+          suppress_health_check=[HealthCheck.function_scoped_fixture, HealthCheck.too_slow])
+@given(K=st.one_of(st.integers(1, 100), st.sampled_from([31, 32, 33, 63, 64, 65, 95, 96, 97, 8191, 8192, 8193,
+                                                         10000, 16447, 20000])),
+       seed=st.integers(0, 2 ** 31 - 1))
+@example(K=10000, seed=1)
+@example(K=16384 + 37, seed=2)
+def test_qfed_hs_recurrence_bit_exact(gpu_device, K, seed):
+    """optimizers.py:96-98: hs = 0; hs = hs + (c1[k] * fp32(sqnorm[k]) + c2[k]) in arrival order, fp32 — the device
+    recurrence (k_qfed_hs, slabs of 8192 terms, batched LDS reads) gives the host's bits for any K."""
+    from fedscale_amd import kernels as kx
+
+    rng = np.random.default_rng(seed)
+    sq = rng.uniform(0.0, 50.0, size=K) * rng.uniform(0.5, 2.0, size=K)
+    c1 = rng.uniform(0.1, 3.0, size=K).astype(np.float32)
+    c2 = rng.uniform(0.0, 40.0, size=K).astype(np.float32)
+    hs = torch.zeros(2, device="cuda")
+    kx.qfed_hs(torch.from_numpy(sq).cuda(), torch.from_numpy(c1).cuda(), torch.from_numpy(c2).cuda(), K, hs)
+    s32 = sq.astype(np.float32)
+    h = np.float32(0)
+    for k in range(K):
+        h = np.float32(h + np.float32(c1[k] * s32[k] + c2[k]))
+    got = hs.cpu().numpy()
+    assert got[0] == h and got[1] == np.float32(h + np.float32(1e-10))
