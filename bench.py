@@ -656,9 +656,10 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend, res
 
         n, t0 = 0, time.perf_counter()
         while n < 3 or (world == 1 and time.perf_counter() - t0 < WARMUP_S):
-            w.step()
+            for _ in range(4):  # batches of 4 rounds queued back to back, as the timed rounds are
+                w.step()
+                n += 1
             torch.cuda.synchronize(dev)
-            n += 1
         warmup = n
     else:
         for _ in range(warmup):
@@ -678,7 +679,8 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend, res
     _sync_all(dev, world)
     wall = time.perf_counter() - t0
     w.card = sampler.stop().summary()
-    kern_ms = float(np.mean([e[0].elapsed_time(e[1]) for e in evs]))
+    w.step_ms = [e[0].elapsed_time(e[1]) for e in evs]  # each timed round's dominant-kernel ms (this rank)
+    kern_ms = float(np.mean(w.step_ms))
     w.split_ms = None
     if split:  # (mean of k_reduce's launches, mean of k_yogi_step) per step, max over ranks
         w.split_ms = _max_over_ranks([float(np.mean([e[0].elapsed_time(e[2]) for e in evs])),
@@ -1044,6 +1046,7 @@ def main():
     (wall, kern_ms_max), kern_ms, kern_ms_ranks = time_workload(w, args.steps, args.warmup, dev, world,
                                                                  args.dist_backend, rest_s=HEADLINE_REST_S)
     warmup_used = w.warmup_rounds  # --warmup -1: the count the auto warmup ran
+    step_ms = list(w.step_ms)
     pg_world = dist.get_world_size() if world > 1 else 1
     strong = not weak and not w.cmode
     card_state = {"before_timed_region": w.card_before, "timed_region": w.card, "rest_s": w.rest_s}
@@ -1170,6 +1173,7 @@ def main():
                                      "fedyogi": "k_reduce (fa_reduce FA_FINALIZE) + k_yogi_step"}[policy]),
                          "alg_bytes_per_launch": alg_bytes / launches, "launches_per_step": launches,
                          "resident_clients": resident, "kernel_ms_per_launch": kern_ms_max / launches,
+                         "kernel_ms_per_launch_by_round": [round(x / launches, 4) for x in step_ms],
                          "traffic_key": "profiles/pmc_traffic.json entries[workload|C<resident_clients>|"
                                         "L<launches_per_step>|<build_id>] (null: no PMC pass of this shape and build)"},
             "card_state": card_state,
