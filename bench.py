@@ -670,7 +670,7 @@ def time_workload(w: Workload, steps: int, warmup: int, dev, world, backend, res
     from fedscale_amd.cardstate import CardSampler
 
     w.card_before = CardSampler(dev).read_once()
-    sampler = CardSampler(dev, period_s=0.02)
+    sampler = CardSampler(dev, period_s=0.02, process=True)  # a child process: no GIL contention with the launches
     _sync_all(dev, world)
     sampler.start()
     t0 = time.perf_counter()
@@ -1077,7 +1077,7 @@ def main():
             from fedscale_amd.state import spmd_rccl_probe
 
             try:
-                rccl_probe = spmd_rccl_probe(local_dev)
+                rccl_probe = spmd_rccl_probe(local_dev, group=cpu_group)
             except Exception as e:  # reported, never fatal
                 rccl_probe = {"error": f"{type(e).__name__}: {e}"}
         else:

@@ -12,7 +12,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FEDAGG_LIB", os.path.join(_HERE, "libfedagg.so"))
-ABI_VERSION = 4  # fedagg.hip FA_ABI_VERSION
+ABI_VERSION = 5  # fedagg.hip FA_ABI_VERSION
 
 FA_ACCUMULATE = 1
 FA_FINALIZE = 2
@@ -37,6 +37,8 @@ SIGNATURES = {
     "fa_build_defs": (ctypes.c_char_p, []),
     "fa_last_error_string": (ctypes.c_char_p, []),
     "fa_pointer_kind": (_i32, [_c_void_p]),
+    "fa_unranged_operands": (_i64, []),
+    "fa_set_strict_operands": (_i32, [_i32]),
     "fa_reduce": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _f32, _i32, _c_void_p]),
     "fa_reduce_mirror": (_i32, [_c_void_p, _i64, _i32, _i64, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _f32, _i32,
                                 _c_void_p]),
@@ -147,6 +149,8 @@ def load(path: str = None, tree: str = None):
         if v != ABI_VERSION:
             raise FedAggError(f"{path}: ABI version {v}, expected {ABI_VERSION}")
         info = check_build(lib, path, tree)
+        if os.environ.get("FEDAGG_STRICT_OPERANDS", "") not in ("", "0"):
+            lib.fa_set_strict_operands(1)  # refuse device operands whose extent HIP cannot report (fa_device.h)
         if tree is None:
             _lib, _info = lib, info
         return lib
@@ -156,6 +160,16 @@ def build_info() -> dict:
     """{path, build_id, defs, verified_against} of the loaded library (loads it)."""
     load()
     return dict(_info)
+
+
+def operand_stats() -> dict:
+    """{unranged, strict}: device operands accepted so far without an extent check (HIP reports no range for VMM /
+    expandable segments; fa_unranged_operands) and whether such operands are refused instead
+    (fa_set_strict_operands, env FEDAGG_STRICT_OPERANDS=1)."""
+    lib = load()
+    prev = lib.fa_set_strict_operands(0)
+    lib.fa_set_strict_operands(prev)
+    return {"unranged": int(lib.fa_unranged_operands()), "strict": bool(prev)}
 
 
 def call(name: str, *args):

@@ -57,10 +57,16 @@ def _level(text):
 
 
 class CardSampler:
-    """Samples the card every ``period_s`` on a daemon thread between ``start()`` and ``stop()``."""
+    """Samples the card every ``period_s`` between ``start()`` and ``stop()``: on a daemon thread, or with
+    ``process=True`` in a child process (``python -m fedscale_amd.cardstate``), so no sysfs read or parsing competes
+    for the GIL with the host thread that launches a timed region's kernels.  The child stamps its
+    samples with the same monotonic clock (``time.perf_counter`` is CLOCK_MONOTONIC on Linux), so ``summary``
+    windows work alike in both modes."""
 
-    def __init__(self, dev, period_s: float = 0.1):
+    def __init__(self, dev, period_s: float = 0.1, process: bool = False):
         self.period = period_s
+        self.process = process
+        self._proc = None
         self.pci = _pci_dir(dev)
         self.files = {}
         self.missing = []
@@ -120,17 +126,46 @@ class CardSampler:
             self._stop.wait(self.period)
 
     def start(self):
+        if self.files and self.process:
+            import json
+            import subprocess
+            import sys
+
+            root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+            spec = json.dumps({"period": self.period, "files": {k: p for k, (p, _) in self.files.items()}})
+            self._proc = subprocess.Popen([sys.executable, "-m", "fedscale_amd.cardstate", spec], cwd=root,
+                                          stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL,
+                                          text=True)
+            self._proc.stdout.readline()  # "ready": the child samples from here on
         self.t0 = time.perf_counter()
-        if self.files:
+        if self.files and not self.process:
             self._t = threading.Thread(target=self._run, name="card-sampler", daemon=True)
             self._t.start()
         return self
 
     def stop(self):
+        self.t1 = time.perf_counter()
         self._stop.set()
         if self._t is not None:
             self._t.join(timeout=2)
-        self.t1 = time.perf_counter()
+        if self._proc is not None:
+            try:
+                out, _ = self._proc.communicate("stop\n", timeout=5)
+            except Exception:
+                self._proc.kill()
+                out, _ = self._proc.communicate()
+            self._proc = None
+            convs = {k: c for k, (_, c) in self.files.items()}
+            for line in out.splitlines():
+                parts = line.split("\t", 2)
+                if len(parts) != 3 or parts[1] not in convs:
+                    continue
+                try:
+                    v = convs[parts[1]](parts[2].replace("\\n", "\n"))
+                except ValueError:
+                    v = None
+                if v is not None:
+                    self.samples[parts[1]].append((float(parts[0]), v))
         return self
 
     def __enter__(self):
@@ -164,3 +199,33 @@ class CardSampler:
 def snapshot(dev) -> dict:
     """One reading of every source (the card's state before a region)."""
     return CardSampler(dev).read_once()
+
+
+def _child(spec: str) -> int:
+    """The process-mode sampler: read the files every period, print "t<TAB>key<TAB>raw text" lines, stop on stdin."""
+    import json
+    import select
+    import sys
+
+    cfg = json.loads(spec)
+    period, files = float(cfg["period"]), cfg["files"]
+    out = []
+    print("ready", flush=True)
+    while True:
+        now = time.perf_counter()
+        for k, path in files.items():
+            t = _read(path)
+            if t is not None:
+                out.append("%.6f\t%s\t%s" % (now, k, t.strip().replace("\n", "\\n")))
+        r, _, _ = select.select([sys.stdin], [], [], period)
+        if r:
+            break
+    sys.stdout.write("\n".join(out) + "\n")
+    sys.stdout.flush()
+    return 0
+
+
+if __name__ == "__main__":
+    import sys
+
+    sys.exit(_child(sys.argv[1]))

@@ -190,6 +190,11 @@ class ShardedModelAdapter(TorchModelAdapter):
         page = 4096
         a0, a1 = lo // page * page, -(-(lo + n) // page) * page  # whole pages of the payload's own mapping
         self._release_registrations(block=False)
+        if a0 in self._regs and a1 > self._regs[a0][2]:
+            # the first page is registered, but by an earlier payload whose registration ends before this one does:
+            # its tail pages are not registered, so this upload takes the gather
+            self.registration_fallbacks += 1
+            return None
         if a0 not in self._regs:
             # two payloads next to each other on the heap can share a boundary page, and a range already registered
             # cannot be registered again: this upload takes the gather, the next ones are tried afresh

@@ -23,6 +23,13 @@
 #include "../../include/fedagg.h"
 
 extern "C" __attribute__((visibility("hidden"))) int fa_internal_set_error(int code, const char* msg);
+// Operands HIP reports no address range for (round 6).  Host memory: its extent comes from the library's
+// own fa_host_register registry (ingress_dma.cpp); *end = one past the registration holding p, 0 if none does.
+extern "C" __attribute__((visibility("hidden"))) int fa_internal_registration_end(const void* p, uintptr_t* end);
+// Device memory (VMM / expandable segments): no extent can be had; each acceptance is counted process-wide
+// (fa_unranged_operands) and, with fa_set_strict_operands(1), refused instead.
+extern "C" __attribute__((visibility("hidden"))) void fa_internal_note_unranged(void);
+extern "C" __attribute__((visibility("hidden"))) int fa_internal_strict_operands(void);
 
 // device of the entry point running on this thread (-1 outside any scope)
 inline thread_local int fa_t_dev = -1;
@@ -149,11 +156,24 @@ class DevScope {
     void* base = nullptr;
     size_t size = 0;
     if (hipMemGetAddressRange((hipDeviceptr_t*)&base, &size, (hipDeviceptr_t)p) != hipSuccess || !base) {
-      // The type and device checks above have passed: the pointer IS memory of this GPU (or mapped pinned memory
-      // where the header allows it).  HIP reports no range for some allocators (hipHostRegister'd memory, VMM /
-      // expandable segments), so only the extent check is skipped here; nothing is cached for this pointer.
+      // The type and device checks above have passed, but HIP reports no range (hipHostRegister'd memory, VMM /
+      // expandable segments).  Host memory takes its extent from the library's own registrations; host memory
+      // nobody registered through the library has no known extent and is refused.  Device memory has none either:
+      // it is accepted and counted (fa_unranged_operands), or refused under fa_set_strict_operands(1).
       (void)hipGetLastError();
+      if (host == 1) {
+        uintptr_t end = 0;
+        if (!fa_internal_registration_end(p, &end) || end <= a)
+          return operr(name, "%s is pinned host memory of unknown extent (HIP reports no range and it is not a "
+                             "fa_host_register registration)", 0);
+        if (bytes > end - a) return operr(name, "%s extends %llu bytes past the end of its registration", bytes - (end - a));
+        return FA_OK;
+      }
+      if (fa_internal_strict_operands())
+        return operr(name, "%s is device memory HIP reports no range for (VMM / expandable segments); its extent "
+                           "cannot be checked and strict operand checks are on (fa_set_strict_operands)", 0);
       ++unranged_;
+      fa_internal_note_unranged();
       return FA_OK;
     }
     const Range r{(uintptr_t)base, (uintptr_t)base + size, host};

@@ -36,7 +36,7 @@
 //    entry point resolves its device from the stream / output pointer (fa_device.h)
 // 3: fa_qfed_accumulate takes the workspace's size, fa_qfed_workspace_bytes the call's (ld, P) (deferred gathers)
 // 4: fa_build_id / fa_build_defs, fa_rccl_comm_info
-#define FA_ABI_VERSION 4
+#define FA_ABI_VERSION 5
 
 // The build id (fedscale_amd/buildinfo.py): a hash of the sources, headers and flags this library was compiled
 // from, passed in by the build.  _native.load() recomputes it from the tree and refuses a library that differs.
@@ -88,6 +88,19 @@ extern "C" __attribute__((visibility("hidden"))) int fa_internal_set_error(int c
   snprintf(g_err, sizeof(g_err), "%s", msg);
   return code;
 }
+
+// operands accepted without an extent check (device memory HIP reports no range for), process-wide; and the switch
+// that refuses them instead (fa_device.h, round 6)
+static std::atomic<int64_t> g_unranged{0};
+static std::atomic<int> g_strict_operands{0};
+extern "C" __attribute__((visibility("hidden"))) void fa_internal_note_unranged(void) {
+  g_unranged.fetch_add(1, std::memory_order_relaxed);
+}
+extern "C" __attribute__((visibility("hidden"))) int fa_internal_strict_operands(void) {
+  return g_strict_operands.load(std::memory_order_relaxed);
+}
+extern "C" int64_t fa_unranged_operands(void) { return g_unranged.load(std::memory_order_relaxed); }
+extern "C" int fa_set_strict_operands(int32_t on) { return g_strict_operands.exchange(on ? 1 : 0); }
 
 extern "C" int fa_abi_version(void) { return FA_ABI_VERSION; }
 extern "C" const char* fa_build_id(void) { return fa_build_marker + sizeof("FA_BUILD_ID=") - 1; }

@@ -32,6 +32,19 @@ bool registered(const void* p, uint64_t n) {
 }
 }  // namespace
 
+// fa_device.h: the extent of registered host memory, which hipMemGetAddressRange does not report
+extern "C" __attribute__((visibility("hidden"))) int fa_internal_registration_end(const void* p, uintptr_t* end) {
+  const uintptr_t a = (uintptr_t)p;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (const auto& r : g_regs)
+    if (a >= r.first && a < r.second) {
+      *end = r.second;
+      return 1;
+    }
+  *end = 0;
+  return 0;
+}
+
 extern "C" int fa_host_register(void* p, int64_t nbytes) {
   if (!p || nbytes <= 0) return fa_internal_set_error(FA_E_ARG, "fa_host_register: NULL pointer or empty range");
   const hipError_t e = hipHostRegister(p, (size_t)nbytes, hipHostRegisterDefault);

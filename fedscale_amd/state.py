@@ -334,20 +334,27 @@ def comm_info(comm, n_local: int) -> dict:
     return {"count": cnt.value, "ranks": list(ranks), "devices": list(devs)}
 
 
-def spmd_rccl_probe(device_index: int, group=None) -> dict:
+def spmd_rccl_probe(device_index: int, group=None, timeout_s: float = 90.0) -> dict:
     """One process per GPU (torch.distributed initialised): open an RCCL communicator of our own over the ranks
     (fa_rccl_unique_id on rank 0, broadcast through the process group, fa_rccl_init_rank on every rank), ask RCCL
     for its rank count, rank and device, gather those to every rank and close it.  What a multi-GPU record shows
-    as "RCCL saw N ranks"."""
+    as "RCCL saw N ranks".
+
+    Collective-safe on every path: ncclCommInitRank blocks until all ranks have joined, so each rank
+    runs its part in a child process (``fedscale_amd.rccl_probe``) under ``timeout_s``; a rank whose init fails or
+    hangs is killed at the deadline, and every rank then reaches the same all_gather of (ok, result | error), so the
+    ranks always leave together, with the failures named."""
     import ctypes
+    import os
+    import subprocess
+    import sys
 
     import torch.distributed as dist
 
     from . import _native
 
     rank, world = dist.get_rank(group), dist.get_world_size(group)
-    # every rank must reach ncclCommInitRank or none may (it blocks until all nranks have joined): agree first on
-    # RCCL being loadable everywhere and on rank 0's id, and skip together otherwise
+    # agree first on RCCL being loadable everywhere and on rank 0's id, and skip together otherwise
     avail = [None] * world
     dist.all_gather_object(avail, bool(_native.load().fa_rccl_available()), group=group)
     if not all(avail):
@@ -363,18 +370,25 @@ def spmd_rccl_probe(device_index: int, group=None) -> dict:
     dist.broadcast_object_list(msg, src=0, group=group)
     if not isinstance(msg[0], bytes):
         return {"error": "fa_rccl_unique_id on rank 0: %s" % msg[0]}
-    ctypes.memmove(idbuf, msg[0], 128)
-    h = ctypes.c_void_p()
-    _native.call("fa_rccl_init_rank", world, idbuf, rank, device_index, ctypes.byref(h))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "fedscale_amd.rccl_probe", "--nranks", str(world), "--rank", str(rank),
+           "--device", str(device_index), "--id", msg[0].hex()]
     try:
-        mine = comm_info(h, 1)
-    finally:
-        _native.call("fa_rccl_destroy", h)
+        r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=timeout_s)
+        lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+        mine = __import__("json").loads(lines[-1]) if lines else {
+            "ok": False, "error": "rc %s: %s" % (r.returncode, r.stderr[-300:])}
+    except subprocess.TimeoutExpired:
+        mine = {"ok": False, "error": f"no result within {timeout_s:g} s (ncclCommInitRank did not complete)"}
     every = [None] * world
-    dist.all_gather_object(every, (mine["count"], mine["ranks"][0], mine["devices"][0]), group=group)
-    return {"count": every[0][0], "counts_agree": all(e[0] == every[0][0] for e in every),
-            "rank_of_process": [e[1] for e in every], "device_of_rank": [e[2] for e in every],
-            "source": "fa_rccl_init_rank + fa_rccl_comm_info (ncclCommCount / ncclCommUserRank / ncclCommCuDevice)"}
+    dist.all_gather_object(every, mine, group=group)  # every rank gets here, whatever its child did
+    bad = {i: e.get("error") for i, e in enumerate(every) if not e.get("ok")}
+    if bad:
+        return {"error": "RCCL probe failed on ranks %s" % sorted(bad), "rank_errors": bad}
+    return {"count": every[0]["count"], "counts_agree": all(e["count"] == every[0]["count"] for e in every),
+            "rank_of_process": [e["user_rank"] for e in every], "device_of_rank": [e["cu_device"] for e in every],
+            "source": "fa_rccl_init_rank + fa_rccl_comm_info (ncclCommCount / ncclCommUserRank / ncclCommCuDevice), "
+                      "one child process per rank with a %g s deadline" % timeout_s}
 
 
 class DeviceGroup:

@@ -65,6 +65,14 @@ const char* fa_last_error_string(void);
 const char* fa_build_id(void);
 const char* fa_build_defs(void);
 
+/* Operand extents HIP cannot report (ABI 5).  Device memory in VMM / expandable segments has no address range, so
+ * its extent cannot be checked: such an operand is accepted after its type and device checks and counted;
+ * fa_unranged_operands() returns that count for the process, and fa_set_strict_operands(1) refuses such operands
+ * with FA_E_ARG instead (returns the previous setting).  Host memory without a range is accepted only inside a
+ * fa_host_register registration, extent included.  No reference counterpart. */
+int64_t fa_unranged_operands(void);
+int fa_set_strict_operands(int32_t on);
+
 /* What a pointer is to the GPU: 0 device memory (or NULL), 1 pinned host memory the GPU reads at the same
  * address (hipHostMalloc, torch pin_memory), -1 anything else (pageable, unregistered, managed) — no entry point
  * hands such a pointer to a kernel: fa_reduce, fa_reduce_mirror and fa_side_accumulate reject it with FA_E_ARG.

@@ -19,6 +19,22 @@ extern "C" int fa_internal_set_error(int code, const char* msg) {
   return code;
 }
 
+// the library's hooks (fedagg.hip / ingress_dma.cpp): a registry of fa_host_register ranges, the unranged counter and
+// the strict switch
+static std::vector<std::pair<uintptr_t, uintptr_t>> g_regs;
+static int g_unranged = 0, g_strict = 0;
+extern "C" int fa_internal_registration_end(const void* p, uintptr_t* end) {
+  for (const auto& r : g_regs)
+    if ((uintptr_t)p >= r.first && (uintptr_t)p < r.second) {
+      *end = r.second;
+      return 1;
+    }
+  *end = 0;
+  return 0;
+}
+extern "C" void fa_internal_note_unranged(void) { ++g_unranged; }
+extern "C" int fa_internal_strict_operands(void) { return g_strict; }
+
 static int launched = 0;
 
 // like fa_reduce: x may be pinned host memory, a / out must be device memory of the call's GPU
@@ -120,13 +136,32 @@ int main() {
   mockhip::add(reg, K * ld * 4, hipMemoryTypeHost, 0, /*ranged=*/false);
   const int l0 = launched;
   rc = entry_reduce(vmm0, K, ld, P, a0, out0, s0);
-  expect(rc == FA_OK && launched == l0 + 1, "device memory without a HIP range (VMM segment): accepted");
+  expect(rc == FA_OK && launched == l0 + 1 && g_unranged == 1,
+         "device memory without a HIP range (VMM segment): accepted and counted");
   rc = entry_reduce(vmm1, K, ld, P, a0, out0, s0);
   expect(rc == FA_E_ARG && has("x is memory of device 1"), "rangeless memory of another device: still FA_E_ARG");
+  g_strict = 1;
+  rc = entry_reduce(vmm0, K, ld, P, a0, out0, s0);
+  expect(rc == FA_E_ARG && launched == l0 + 1 && has("strict operand checks"),
+         "strict operand checks: rangeless device memory refused");
+  g_strict = 0;
+  // rangeless host memory: only inside a fa_host_register registration, extent checked against it
+  rc = entry_reduce(reg, K, ld, P, a0, out0, s0);
+  expect(rc == FA_E_ARG && launched == l0 + 1 && has("unknown extent"),
+         "rangeless pinned memory the library did not register: FA_E_ARG");
+  g_regs.emplace_back((uintptr_t)reg, (uintptr_t)reg + K * ld * 4);
   rc = entry_reduce(reg, K, ld, P, a0, out0, s0);
   expect(rc == FA_OK && launched == l0 + 2, "registered pinned memory without a range where host memory is allowed");
+  rc = entry_reduce(reg, K + 1, ld, P, a0, out0, s0);
+  expect(rc == FA_E_ARG && launched == l0 + 2 && has("past the end of its registration"),
+         "an undersized registered buffer (one row short): FA_E_ARG");
+  g_regs.back().second -= 4096;
+  rc = entry_reduce(reg, K, ld, P, a0, out0, s0);
+  expect(rc == FA_E_ARG && has("past the end of its registration"), "registration shorter than the rows: FA_E_ARG");
+  g_regs.back().second += 4096;
   rc = entry_reduce(x0, K, ld, P, (const float*)reg, out0, s0);
   expect(rc == FA_E_ARG && has("a is pinned host memory"), "rangeless pinned memory where device memory is required");
+  expect(g_unranged == 1, "only the rangeless device operand was counted");
 
   // pointer tables: 96 tensors in 3 segments of device 1 -> 3 queries per table, not 96
   const int T = 96;

@@ -179,3 +179,90 @@ def rccl_probe_agreement_worker(rank, world, port, unavailable_rank):
         assert "skipped" in r and str(unavailable_rank) in r["skipped"], r
     finally:
         dist.destroy_process_group()
+
+
+def rccl_probe_failure_worker(rank, world, port, failing_rank):
+    """spmd_rccl_probe when ONE rank's ncclCommInitRank fails or hangs.  Each rank's part runs in a child
+    process under a deadline; here the child is simulated (the CPU has no GPU): the failing rank's times out, the
+    others report success.  Every rank must return — none blocks in a collective the failing rank never enters — and
+    every rank must name the failing rank."""
+    import json
+    import subprocess
+
+    from fedscale_amd import _native
+    from fedscale_amd.state import spmd_rccl_probe
+
+    _init(rank, world, port)
+    try:
+        lib = _native.load()
+
+        class _Lib:
+            def __getattr__(self, name):
+                return getattr(lib, name)
+
+            @staticmethod
+            def fa_rccl_available():
+                return 1
+
+        orig_load, orig_call, orig_run = _native.load, _native.call, subprocess.run
+
+        def call(name, *a):
+            if name == "fa_rccl_unique_id":
+                return 0  # the id buffer stays zeros: the simulated children never read it
+            return orig_call(name, *a)
+
+        def run(cmd, **kw):
+            assert "fedscale_amd.rccl_probe" in cmd and kw.get("timeout"), cmd
+            if rank == failing_rank:
+                raise subprocess.TimeoutExpired(cmd, kw["timeout"])
+            out = {"rank": rank, "ok": True, "count": world, "user_rank": rank, "cu_device": rank}
+            return subprocess.CompletedProcess(cmd, 0, json.dumps(out) + "\n", "")
+
+        _native.load, _native.call, subprocess.run = (lambda *a, **k: _Lib()), call, run
+        try:
+            r = spmd_rccl_probe(rank, timeout_s=5)
+        finally:
+            _native.load, _native.call, subprocess.run = orig_load, orig_call, orig_run
+        assert "error" in r and list(r["rank_errors"]) == [failing_rank], r
+        assert "no result within" in r["rank_errors"][failing_rank], r
+    finally:
+        dist.destroy_process_group()
+
+
+def rccl_probe_success_worker(rank, world, port):
+    """spmd_rccl_probe with every (simulated) child succeeding: every rank gets the same table of RCCL's view."""
+    import json
+    import subprocess
+
+    from fedscale_amd import _native
+    from fedscale_amd.state import spmd_rccl_probe
+
+    _init(rank, world, port)
+    try:
+        lib = _native.load()
+
+        class _Lib:
+            def __getattr__(self, name):
+                return getattr(lib, name)
+
+            @staticmethod
+            def fa_rccl_available():
+                return 1
+
+        orig_load, orig_call, orig_run = _native.load, _native.call, subprocess.run
+
+        def call(name, *a):
+            return 0 if name == "fa_rccl_unique_id" else orig_call(name, *a)
+
+        def run(cmd, **kw):
+            out = {"rank": rank, "ok": True, "count": world, "user_rank": rank, "cu_device": rank}
+            return subprocess.CompletedProcess(cmd, 0, json.dumps(out) + "\n", "")
+
+        _native.load, _native.call, subprocess.run = (lambda *a, **k: _Lib()), call, run
+        try:
+            r = spmd_rccl_probe(rank, timeout_s=5)
+        finally:
+            _native.load, _native.call, subprocess.run = orig_load, orig_call, orig_run
+        assert r["count"] == world and r["counts_agree"] and r["rank_of_process"] == list(range(world)), r
+    finally:
+        dist.destroy_process_group()

@@ -3,6 +3,8 @@ found by label, converted (µW -> W, m°C -> °C, the pp_dpm level marked '*'), 
 that exposes none of them gives a summary that says so instead of raising."""
 import time
 
+import pytest
+
 from fedscale_amd import cardstate
 
 
@@ -20,10 +22,11 @@ def _tree(tmp_path, power=1_180_000_000, junction=52_000, mem=76_000, mclk="0: 2
     return pci
 
 
-def test_sources_found_and_converted(tmp_path, monkeypatch):
+@pytest.mark.parametrize("process", [False, True])
+def test_sources_found_and_converted(tmp_path, monkeypatch, process):
     pci = _tree(tmp_path)
     monkeypatch.setattr(cardstate, "_pci_dir", lambda dev: str(pci))
-    s = cardstate.CardSampler("cuda:0", period_s=0.01)
+    s = cardstate.CardSampler("cuda:0", period_s=0.01, process=process)
     one = s.read_once()
     assert one == {"power_w": 1180.0, "temp_junction_c": 52.0, "temp_mem_c": 76.0, "mclk_mhz": 2000.0,
                    "sclk_mhz": 2394.0}
@@ -34,10 +37,11 @@ def test_sources_found_and_converted(tmp_path, monkeypatch):
     assert "missing" not in summ
 
 
-def test_windowed_summary_follows_the_samples(tmp_path, monkeypatch):
+@pytest.mark.parametrize("process", [False, True])
+def test_windowed_summary_follows_the_samples(tmp_path, monkeypatch, process):
     pci = _tree(tmp_path)
     monkeypatch.setattr(cardstate, "_pci_dir", lambda dev: str(pci))
-    s = cardstate.CardSampler("cuda:0", period_s=0.01).start()
+    s = cardstate.CardSampler("cuda:0", period_s=0.01, process=process).start()
     time.sleep(0.05)
     t_mid = time.perf_counter()
     (pci / "hwmon" / "hwmon7" / "temp3_input").write_text("80000")

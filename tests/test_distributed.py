@@ -58,3 +58,11 @@ def test_cpu_client_sharded_reduction_world8(name):
 
 def test_rccl_probe_skips_on_every_rank_together():
     mp.spawn(dist_workers.rccl_probe_agreement_worker, args=(3, _port(), 1), nprocs=3, join=True)
+
+
+def test_rccl_probe_failing_rank_does_not_hang_the_others():
+    mp.spawn(dist_workers.rccl_probe_failure_worker, args=(3, _port(), 1), nprocs=3, join=True)
+
+
+def test_rccl_probe_gathers_every_ranks_view():
+    mp.spawn(dist_workers.rccl_probe_success_worker, args=(2, _port()), nprocs=2, join=True)

@@ -219,7 +219,7 @@ def test_pageable_operand_in_every_position_is_rejected_before_any_launch(gpu_de
     host_or_query = {"fa_abi_version", "fa_build_id", "fa_build_defs", "fa_last_error_string", "fa_pointer_kind",
                      "fa_reduce_launches", "fa_qfed_launches", "fa_qfed_max_chunk", "fa_qfed_workspace_bytes", "fa_host_gather",
                      "fa_pickle_strip", "fa_dp_workspace_bytes", "fa_host_register", "fa_host_unregister",
-                     "fa_h2d_pieces"}  # (fa_h2d_pieces: its own test below)
+                     "fa_h2d_pieces", "fa_unranged_operands", "fa_set_strict_operands"}  # (fa_h2d_pieces: below)
     rccl = {n for n in exported if n.startswith("fa_rccl_")}
     assert exported - host_or_query - rccl == {c.name for c in cases}
 
@@ -372,7 +372,17 @@ kx.reduce(x, K, P, out, denom=float(np.float32(K)), finalize=True)
 got = out[:P].cpu().numpy()
 want = fedavg_flat(h[:, :P])[:P]
 assert np.array_equal(got, want), "mean differs"
-print("OK", torch.cuda.memory_stats().get("num_alloc_retries", 0))
+from fedscale_amd import _native
+st = _native.operand_stats()
+if st["unranged"] > 0:  # HIP gave no range for the segment: counted, and refused under strict checks (ABI 5)
+    _native.load().fa_set_strict_operands(1)
+    try:
+        kx.reduce(x, K, P, out, denom=float(np.float32(K)), finalize=True)
+        raise SystemExit("strict operand checks accepted a rangeless operand")
+    except _native.FedAggError as e:
+        assert "strict operand checks" in str(e), e
+    _native.load().fa_set_strict_operands(0)
+print("OK", st["unranged"], torch.cuda.memory_stats().get("num_alloc_retries", 0))
 """
 
 
@@ -414,5 +424,42 @@ def test_host_registered_pinned_x_is_accepted(gpu_device):
                      _native.FA_FINALIZE, st)
         torch.cuda.synchronize()
         assert np.array_equal(out[:P].cpu().numpy(), fedavg_flat(h[:, :P])[:P])
+        # one row more than the registration holds: refused before anything is queued
+        st = torch.cuda.current_stream().cuda_stream
+        with pytest.raises(_native.FedAggError, match="past the end of its registration|past the end of its allocation"):
+            _native.call("fa_reduce", h.ctypes.data, ld, K + 1, P, None, None, out.data_ptr(),
+                         float(np.float32(K)), _native.FA_FINALIZE, st)
     finally:
         _native.call("fa_host_unregister", h.ctypes.data)
+
+
+def test_host_memory_registered_outside_the_library_is_refused(gpu_device):
+    """pinned host memory HIP reports no range for and that no fa_host_register call covers has no known
+    extent, so it is refused (FA_E_ARG) rather than handed to a kernel that might read past it."""
+    import ctypes
+
+    import numpy as np
+
+    from fedscale_amd import _native
+
+    K, P, ld = 3, 8192, 8192
+    page = 4096
+    raw = np.zeros(K * ld * 4 + 2 * page, dtype=np.uint8)
+    off = (-raw.ctypes.data) % page
+    h = raw[off:off + K * ld * 4].view(np.float32).reshape(K, ld)
+    hip = ctypes.CDLL("libamdhip64.so")
+    assert hip.hipHostRegister(ctypes.c_void_p(h.ctypes.data), ctypes.c_size_t(h.nbytes), 0) == 0
+    try:
+        out = torch.empty(ld, device="cuda:0")
+        st = torch.cuda.current_stream().cuda_stream
+        lib = _native.load()
+        rc = lib.fa_reduce(h.ctypes.data, ld, K, P, None, None, out.data_ptr(), float(np.float32(K)),
+                           _native.FA_FINALIZE, st)
+        msg = lib.fa_last_error_string().decode()
+        if rc == 0:  # this HIP reports a range for registered memory: the extent was checked against it
+            torch.cuda.synchronize()
+            assert "unknown extent" not in msg
+        else:
+            assert rc == -1 and "unknown extent" in msg, msg
+    finally:
+        hip.hipHostUnregister(ctypes.c_void_p(h.ctypes.data))

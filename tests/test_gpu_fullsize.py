@@ -424,3 +424,85 @@ def test_reduce_yogi_balanced_plans_bit_exact(gpu_device, K, P):
         last.copy_(out)
         L = new
     del x
+
+
+def test_c5_one_gpu_bench_shape_k2c17_p100m(gpu_device):
+    """config 5 on ONE GPU exactly as bench.py times it (``Workload`` of c5_qfedavg_k10000_p100M):
+    100 M columns, the resident chunk C the bench picks on this box (0.6 of the free HBM, ≈ 462 clients), K = 2C + 17
+    so the round streams three passes over the chunk (two full, one of 17), the fused FedAvg chain
+    (aggregator.py:497-507) and a workspace holding every column window's partials, so the per-client norms are
+    gathered once per call by k_qfed_gather_win_wave over ≈ 50 windows.  Against the oracle's op order
+    (optimizers.py:73-104): delta, chain, the mean from the chain and the new model bit-exact on sampled columns that
+    include both sides of every chain-window seam; the norms within 1e-9 of fp64 sums over all 100 M columns (the
+    clients of the first, a middle and the last row); hs bit-exact (the fp32 recurrence of :96-98)."""
+    import bench
+    from fedscale_amd import kernels as kx
+    from fedscale_amd import synth
+    from fedscale_amd.bucket import round_up
+    from fedscale_amd.state import ShardGroup
+
+    torch.cuda.empty_cache()
+    P, seed, lr = 100_000_000, 2024, 0.05
+    ld = round_up(P, 64)
+    free, _ = torch.cuda.mem_get_info(gpu_device)
+    C = min(max(1, int(free * bench.MEM_FRACTION) // (4 * ld)), kx.qfed_max_chunk())
+    assert C >= 64, f"only {C} resident clients fit"
+    K = 2 * C + 17
+    w = bench.Workload("qfedavg", K, P, 0, 1, gpu_device, seed, ShardGroup(0, 1), chunk=C,
+                       budget_fraction=bench.MEM_FRACTION)
+    assert w.C == C and len(w.passes) == 3 and w.passes[-1] == (2 * C, 17)
+    assert w.mean_chain and w.qf["chain"] is not None  # several passes: the drop-in's fused chain
+    win = kx.qfed_window(chain=True)
+    nwin = kx.qfed_launches(ld, P, chain=True)
+    assert nwin >= 40  # ≈ 50 column windows per call, gathered once per call
+    assert w.qf["ws"].numel() * 8 >= _native_ws_bytes(C, ld, P)
+    w.step()
+    torch.cuda.synchronize()
+    qf = w.qf
+    seams = np.arange(win, P, win)
+    cols = np.unique(np.concatenate([_sample_cols(P, n=1024, seed=5), seams - 1, seams]))
+    ci = torch.from_numpy(cols).to(gpu_device)
+    L = synth.host_columns(seed, [0], cols, scale_noise=0.0)[0]  # Workload's last: base only
+    np.testing.assert_array_equal(qf["last"][ci].cpu().numpy(), L)
+    rows = synth.host_columns(seed, range(C), cols)  # the resident chunk (client k of the round reads row k % C)
+    alpha = qf["alpha"].cpu().numpy()
+    f32 = np.float32
+    d = acc = None
+    for k in range(K):
+        row = rows[k % C]
+        g = (L - row) / f32(lr)
+        t = alpha[k] * g
+        d = t if d is None else d + t
+        acc = row.copy() if acc is None else acc + row
+    np.testing.assert_array_equal(qf["delta"][ci].cpu().numpy(), d)
+    np.testing.assert_array_equal(qf["chain"][ci].cpu().numpy(), acc)
+    mean = torch.empty(ld, device=gpu_device)
+    kx.reduce(qf["chain"].view(1, ld), 1, P, mean, denom=float(f32(K)), finalize=True)  # mean_from_staging
+    np.testing.assert_array_equal(mean[ci].cpu().numpy(), np.divide(acc, f32(K)))
+    sq = qf["sq"].cpu().numpy()
+    assert np.all(sq > 0)
+    for k in range(C):  # a row read in every pass gives its clients the same norm, bit for bit
+        assert sq[k] == sq[k + C] and (k >= 17 or sq[k] == sq[k + 2 * C])
+    Lfull = qf["last"][:P].cpu().numpy()
+    for j in (0, C // 2, C - 1):
+        row = w.xs[0][j, :P].cpu().numpy()
+        np.testing.assert_array_equal(row[cols], rows[j])
+        g = (Lfull - row) / f32(lr)
+        ref = np.sum((g * g).astype(np.float64))
+        assert abs(sq[j] - ref) <= 1e-9 * ref, (j, sq[j], ref)
+        del row, g
+    c1, c2 = qf["c1"].cpu().numpy(), qf["c2"].cpu().numpy()
+    hs = f32(0.0)
+    for k in range(K):
+        hs = f32(hs + f32(c1[k] * f32(sq[k]) + c2[k]))
+    hs_got = qf["hs"].cpu().numpy()
+    assert hs_got[0] == hs and hs_got[1] == f32(hs + f32(1e-10))
+    np.testing.assert_array_equal(w.out[ci].cpu().numpy(), L - d / f32(hs_got[1]))
+    w.free()
+    del mean
+
+
+def _native_ws_bytes(K, ld, P):
+    from fedscale_amd import _native
+
+    return int(_native.load().fa_qfed_workspace_bytes(K, ld, P))

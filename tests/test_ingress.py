@@ -408,3 +408,45 @@ def test_upload_decoded_on_arrival_by_the_servicer_thread():
     s.device_decode_on_arrival = True
     s.add_event_handler(1, "upload_model", None, payload)
     assert s.deserialize_response(s.server_events_queue[0][3])["client_id"] == 4
+
+
+def test_sharded_registration_reuse_checks_the_end_page(monkeypatch):
+    """an upload whose first payload page an EARLIER registration already covers may reuse that
+    registration only if it ends inside it; a payload that extends past it takes the pinned-row gather (counted in
+    ``registration_fallbacks``) instead of reaching fa_h2d_pieces with unregistered tail pages.  CPU: the adapter's
+    registration bookkeeping alone, the native calls recorded."""
+    import torch
+
+    from fedscale_amd import synth
+    from fedscale_amd.bucket import BucketLayout
+    from fedscale_amd.cloud.internal.sharded_model_adapter import ShardedModelAdapter
+
+    names, shapes = ["a.weight", "b.weight"], [(512, 1024), (512, 1024)]
+    model = synth.LayoutModule(names, shapes, [torch.float32] * 2)
+    L = BucketLayout.from_state_dict(model.state_dict())
+    rng = np.random.default_rng(0)
+    up = {n: rng.standard_normal(s, dtype=np.float32) for n, s in zip(names, shapes)}
+    payload = pickle.dumps({"update_weight": up})
+    dec = ingress.loads(payload)["update_weight"]
+    calls = []
+    monkeypatch.setattr(_native, "call", lambda name, *a: calls.append((name,) + a) or 0)
+
+    class _Pending:  # a registration whose copies are still running
+        events = [type("E", (), {"query": staticmethod(lambda: False)})()]
+
+    ad = ShardedModelAdapter.__new__(ShardedModelAdapter)
+    ad.layout, ad._reg_segs, ad._regs = L, None, {}
+    ad.registered_uploads = ad.registration_fallbacks = 0
+    plan = L.host_gather_plan(L.values_of(dec))
+    buf = np.frombuffer(payload, dtype=np.uint8)
+    a0 = buf.ctypes.data // 4096 * 4096
+    a1 = -(-(buf.ctypes.data + buf.nbytes) // 4096) * 4096
+    # an earlier payload's registration starting on the same page but ending one page short of this one
+    ad._regs[a0] = [b"earlier", [_Pending()], a1 - 4096]
+    assert ad._register(plan) is None
+    assert ad.registration_fallbacks == 1 and not any(c[0] == "fa_host_register" for c in calls)
+    # one that covers the whole payload is reused (no second registration)
+    ad._regs[a0] = [b"earlier", [_Pending()], a1]
+    got = ad._register(plan)
+    assert got is not None and got[2] == a0 and ad.registration_fallbacks == 1
+    assert not any(c[0] == "fa_host_register" for c in calls)
