@@ -94,6 +94,8 @@ def parse():
                                                                      "every CPU leg)")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--no-other-configs", action="store_true", help="skip the side measurements (other_configs)")
+    ap.add_argument("--no-pcie", action="store_true",
+                    help="N > 1: skip the PCIe-inclusive N-link round (pcie_inclusive) rank 0 runs after the timed region")
     ap.add_argument("--no-selfcheck", action="store_true",
                     help="N > 1: skip the in-process multi-GPU drop-in check (fedscale_amd.selfcheck) rank 0 runs "
                          "over all N GPUs after the timed region")
@@ -213,11 +215,16 @@ def cpu_leg(policy: str, K: int, P: int, budget_s: float, seed: int, pool_n: int
     return out
 
 
-def cpu_baseline(K: int, P: int, budget_s: float, seed: int) -> dict:
-    """The headline's CPU leg: the oracle's FedAvg on a K-subsample, extrapolated to K."""
-    leg = cpu_leg("fedavg", K, P, budget_s, seed)
-    return dict({"value": leg["client_updates_per_s"], "unit": "client-updates/s", "cores": 1, "kind": "port",
-                 "sample": (f"oracle FedAvg (numpy, single-threaded) over {leg['accumulate_clients_timed']} of the "
+def cpu_baseline(K: int, P: int, budget_s: float, seed: int, policy: str = "fedavg") -> dict:
+    """The line's CPU leg: the oracle's round of the line's policy on a K-subsample, extrapolated to K (the whole
+    model, at every N: the reference aggregator is one CPU process whatever the GPU count)."""
+    leg = cpu_leg(policy, K, P, budget_s, seed)
+    name = {"fedavg": "FedAvg (numpy, single-threaded)", "fedbuff": "FedAvg accumulate (numpy, single-threaded)",
+            "fedyogi": "FedYoGi (numpy accumulate + torch CPU YoGi step)",
+            "qfedavg": "q-FedAvg (numpy accumulate + torch CPU q-FedAvg step)"}[policy]
+    return dict({"value": leg["client_updates_per_s"], "unit": "client-updates/s", "cores": leg["cores"],
+                 "kind": "port",
+                 "sample": (f"oracle {name} over {leg['accumulate_clients_timed']} of the "
                             f"{K} x {P} fp32 client updates (pool of {leg['pool_buffers']} distinct "
                             f"{4 * P / 1e6:.0f} MB buffers), {leg['accumulate_ms_per_client']:.1f} ms/client + "
                             f"{leg['finalize_ms']:.0f} ms finalize, extrapolated linearly to K={K}")},
@@ -301,60 +308,21 @@ def pcie_inclusive_leg(dev, seed: int, K: int = 64, rounds: int = 6) -> dict:
     pickled upload payloads (CLIENT_EXECUTE_COMPLETION) through the mixin's zero-copy deserialize_response
     (aggregator.py:704), the pinned gather + H2D and the reduce, to get_weights() (D2H egress,
     torch_model_adapter.py:41-47).  25 M fp32 as 10 tensors of 2.5 M (100 MB per update); 8 distinct payloads
-    reused.  Never `value`: it is bound by one PCIe link (PCIe-inclusive rate)."""
-    import pickle
-
-    import numpy as np
+    reused.  Never `value`: it is bound by one PCIe link (PCIe-inclusive rate).  The same rounds as
+    the N > 1 line's ``pcie_inclusive`` (fedscale_amd.inproc_bench.pcie_rounds), on one GPU."""
     import torch
 
-    from fedscale_amd import synth
-    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
     from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+    from fedscale_amd.inproc_bench import headline_model, pcie_rounds
 
-    names, shapes = [f"l{i}.weight" for i in range(10)], [(2500, 1000)] * 10
-    model = synth.LayoutModule(names, shapes, [torch.float32] * 10)
-    adapter = TorchModelAdapter(model, device=dev)
-    agg = DeviceAggregator(adapter)
-    rng = np.random.default_rng(seed)
-    payloads = []
-    for i in range(8):
-        up = {n: t.numpy() + rng.standard_normal(t.shape, dtype=np.float32) * np.float32(0.01)
-              for n, t in model.state_dict().items()}
-        payloads.append(pickle.dumps({"client_id": i, "moving_loss": 1.0, "trained_size": 200, "success": True,
-                                      "utility": 1.0, "update_weight": up, "wall_duration": 0}))
-        del up
-    ts, t_in, t_fin, t_eg = [], [], [], []
-    for r in range(rounds + 1):
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        agg.start_round(K)
-        for k in range(K - 1):
-            agg.on_result(agg.deserialize_response(payloads[k % 8]))
-        t1 = time.perf_counter()
-        agg.on_result(agg.deserialize_response(payloads[(K - 1) % 8]))  # the K-th: its H2D, then the reduce
-        torch.cuda.synchronize(dev)
-        t2 = time.perf_counter()
-        adapter.get_weights()
-        t3 = time.perf_counter()
-        if r:
-            ts.append(t3 - t0)
-            t_in.append(t1 - t0)
-            t_fin.append(t2 - t1)
-            t_eg.append(t3 - t2)
-    s, smin = float(np.median(ts)), float(np.min(ts))
-    tin = float(np.median(t_in))
-    P = adapter.layout.P_full
-    del agg, adapter, payloads
+    adapter = TorchModelAdapter(headline_model(), device=dev)
+    out, _ = pcie_rounds(adapter, K=K, rounds=rounds, seed=seed)
+    del adapter
     torch.cuda.empty_cache()
-    return {"clients": K, "params": P, "round_ms": s * 1e3, "round_ms_min": smin * 1e3,
-            "rounds_ms": [t * 1e3 for t in ts], "client_updates_per_s": K / s, "client_updates_per_s_best": K / smin,
-            "host_to_device_GBps": 4 * K * P / s / 1e9, "host_to_device_GBps_best": 4 * K * P / smin / 1e9,
-            "phases_ms": {"ingress_first_K_minus_1": tin * 1e3, "last_upload_and_reduce": float(np.median(t_fin)) * 1e3,
-                          "egress_get_weights": float(np.median(t_eg)) * 1e3},
-            "ingress_GBps": 4 * (K - 1) * P / tin / 1e9,
-            "note": "from pickled executor payloads: zero-copy deserialize_response, pinned gather + H2D, reduce, "
-                    "get_weights() D2H; median and min of %d rounds after one warm-up round; bound by one PCIe "
-                    "link, never `value`" % rounds}
+    out["note"] = ("from pickled executor payloads: zero-copy deserialize_response, pinned gather + H2D, reduce, "
+                   "get_weights() D2H; median and min of %d rounds after one warm-up round; bound by one PCIe "
+                   "link, never `value`" % rounds)
+    return out
 
 
 def cpu_baseline_c1(seed: int, rounds: int = 300) -> dict:
@@ -869,6 +837,10 @@ def promote_inproc(res: dict, inproc: dict, K: int, steps: int) -> None:
     if not fa or not fa.get("ok") or "inproc_round_ms" not in fa:
         res["value_source"] = "spmd (the in-process drop-in run failed: %s)" % ((fa or inproc).get("error"),)
         return
+    if fa.get("distinct_gpus") is False:  # parts sharing a GPU (a rehearsal): plumbing, never the line's value
+        res["value_source"] = "spmd (the in-process parts share %s GPU(s): plumbing, not promoted)" % (
+            len(set(fa.get("devices", []))) or "one")
+        return
     res["value_spmd"], res["ms_per_step_spmd"] = res["value"], res["ms_per_step"]
     for k in ("scaling_vs_one_gpu", "scaling_vs_one_gpu_incl_reassembly", "value_incl_reassembly",
               "round_ms_incl_reassembly"):
@@ -929,6 +901,92 @@ def run_inproc_bench(world: int, K: int, P: int, backend: str, steps: int = 6, w
         rep["note"] = (f"{world} parts on {len(set(devs))} GPU(s) (backend {backend} rehearsal): plumbing only, "
                        "not an N-GPU rate")
     return rep
+
+
+#: one PCIe link's rate for the PCIe-inclusive round of the headline model on one GPU (profiles/r05_bench_default_n1_final.json
+#: headline_model_pcie_inclusive: 52-54 GB/s end to end, the copy engine's 56-57 GB/s, r01_h2d_probe.json): the
+#: basis of the N-link prediction each N > 1 line carries
+PCIE_LINK_GBPS = 54.0
+
+
+def pcie_prediction(world: int) -> dict:
+    """What the N-GPU PCIe-inclusive round should reach if every GPU's link carries what one link carries alone:
+    N x one link.  The registered ingress reads each payload byte once from host DRAM, so up to
+    8 links (~430 GB/s) stays inside the host's memory bandwidth (2 sockets x 12 channels of DDR5); below
+    N x 54 GB/s, the bound is elsewhere (a shared PCIe switch, one socket's DRAM, the Python ingress loop)."""
+    return {"host_to_device_GBps": world * PCIE_LINK_GBPS, "client_updates_per_s": world * PCIE_LINK_GBPS * 1e9 / 100e6,
+            "basis": "N x %g GB/s (one link's PCIe-inclusive rate at N = 1, DESIGN.md §5/§6)" % PCIE_LINK_GBPS}
+
+
+def run_inproc_pcie(world: int, backend: str, K: int = 64, rounds: int = 6, timeout_s: int = 300) -> dict:
+    """The PCIe-inclusive round over GPUs 0..N-1 in a child process (rank 0, N > 1; fedscale_amd.inproc_bench
+    --pcie): one aggregator process, the executors' pickled payloads registered in place and sliced over the N links
+    (ShardedModelAdapter), reduce on every GPU, get_weights() D2H.  With fewer GPUs than ranks (a gloo rehearsal on
+    one card) the parts share the visible GPUs: plumbing only."""
+    import subprocess
+
+    import torch
+
+    nd = torch.cuda.device_count()
+    devs = [i % max(1, nd) for i in range(world)]
+    cmd = [sys.executable, "-m", "fedscale_amd.inproc_bench", "--devices", ",".join(map(str, devs)), "--pcie",
+           "--clients", str(K), "--rounds", str(rounds)]
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"devices": devs, "ok": False, "error": f"no result within {timeout_s} s"}
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if not lines:
+        return {"devices": devs, "ok": False, "rc": r.returncode, "error": r.stderr[-400:]}
+    rep = json.loads(lines[-1])
+    rep["seconds"] = round(time.perf_counter() - t0, 1)
+    rep["prediction"] = pcie_prediction(world)
+    if rep.get("ok") and rep.get("distinct_gpus"):
+        rep["vs_prediction"] = rep["host_to_device_GBps"] / rep["prediction"]["host_to_device_GBps"]
+    elif rep.get("ok"):
+        rep["note_backend"] = (f"{world} parts on {len(set(devs))} GPU(s) (backend {backend} rehearsal): plumbing only, "
+                               "not an N-link rate")
+    return rep
+
+
+#: fields every line carries (the contract), and what an N > 1 line must carry on top (VERDICT r5 #1: the north
+#: star's CPU baseline beside the 1/2/4/8-GPU figures, and the rate including H2D and D2H copies)
+LINE_FIELDS = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+               "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
+ROOFLINE_FIELDS = ("bound", "achieved", "peak", "unit", "frac", "traffic")
+CPU_BASELINE_FIELDS = ("value", "unit", "cores", "kind", "sample")
+PCIE_FIELDS = ("round_ms", "client_updates_per_s", "host_to_device_GBps", "phases_ms", "parts", "prediction")
+PART_FIELDS = ("device", "params", "host_numa_node", "h2d_GBps_over_ingress")
+
+
+def check_line(res: dict) -> list:
+    """Missing north-star quantities of a bench line ([] = complete).  N = 1: the contract's fields with a non-null
+    cpu_baseline (unless its CPU legs were switched off).  N > 1: also ``cpu_baseline`` (the oracle on rank 0's host
+    cores, same run) and ``pcie_inclusive`` (the N-link round from pickled payloads, every part's link rate and NUMA
+    node, and the prediction it is checked against)."""
+    miss = [k for k in LINE_FIELDS if k not in res]
+    miss += ["roofline." + k for k in ROOFLINE_FIELDS if k not in (res.get("roofline") or {})]
+    cb = res.get("cpu_baseline")
+    if cb is None:
+        if res.get("n_gpus", 1) > 1 or not res.get("cpu_legs_off"):
+            miss.append("cpu_baseline (null)")
+    else:
+        miss += ["cpu_baseline." + k for k in CPU_BASELINE_FIELDS if k not in cb]
+    if res.get("n_gpus", 1) > 1:
+        pc = res.get("pcie_inclusive")
+        if not pc:
+            miss.append("pcie_inclusive")
+        elif not pc.get("ok", True):
+            miss.append("pcie_inclusive (failed: %s)" % pc.get("error"))
+        else:
+            miss += ["pcie_inclusive." + k for k in PCIE_FIELDS if k not in pc]
+            parts = pc.get("parts") or []
+            if len(parts) != res["n_gpus"]:
+                miss.append("pcie_inclusive.parts (%d for %d GPUs)" % (len(parts), res["n_gpus"]))
+            for i, p in enumerate(parts):
+                miss += ["pcie_inclusive.parts[%d].%s" % (i, k) for k in PART_FIELDS if k not in p]
+    return miss
 
 
 def one_gpu_reference(policy, K, P, dev, seed, steps=5, warmup=2) -> dict:
@@ -1091,6 +1149,18 @@ def main():
     w.free()
     del w
 
+    drop_in = None
+    if world == 1 and policy == "fedavg" and not weak and not args.no_other_configs:
+        # the same round through the drop-in (TorchModelAdapter begin_round / apply_round, every launch on the part's
+        # stream) with the N > 1 line's in-process timing (fedscale_amd.inproc_bench): value(N) / value_drop_in(1)
+        # then compares one methodology; outside the timed region, never `value`
+        from fedscale_amd.inproc_bench import run_one
+
+        try:
+            drop_in = run_one(local_dev, K, P, rounds=args.steps, warmup=max(2, min(warmup_used, 8)), seed=args.seed)
+        except Exception as e:  # reported, never fatal
+            drop_in = {"error": f"{type(e).__name__}: {e}"}
+
     other = None
     if not args.no_other_configs and args.config == "headline":
         if world == 1:
@@ -1125,6 +1195,19 @@ def main():
         dist.barrier(group=cpu_group)
         if rank == 0:
             selfcheck = run_selfcheck(world)
+        dist.barrier(group=cpu_group)
+
+    pcie = cpu_base = None
+    if world > 1 and not args.no_pcie:
+        # the north star's two other figures beside the N-GPU one, outside the timed region, the other ranks waiting at
+        # a host-side barrier: the rate including H2D and D2H copies over the N links (one aggregator process, pickled
+        # payloads -> N GPUs -> get_weights), and the reference CPU aggregator (the oracle) on rank 0's host cores
+        _sync_all(dev, world)
+        dist.barrier(group=cpu_group)
+        if rank == 0:
+            pcie = run_inproc_pcie(world, args.dist_backend)
+            if args.cpu_seconds > 0:
+                cpu_base = cpu_baseline(K, P, args.cpu_seconds, args.seed, policy)
         dist.barrier(group=cpu_group)
 
     if rank == 0:
@@ -1180,6 +1263,12 @@ def main():
         }
         if sustained is not None:
             res["sustained"] = sustained
+        if drop_in is not None:
+            res["drop_in_one_gpu"] = drop_in
+            if "round_ms" in drop_in:
+                res["value_drop_in"] = drop_in["client_updates_per_s"]
+                drop_in["note"] = ("the same round through TorchModelAdapter, timed as the N > 1 line's in-process value "
+                                   "(fedscale_amd.inproc_bench): value(N) / value_drop_in(1) is one methodology")
         if split_ms:
             res["roofline"]["kernel_ms_split"] = {"k_reduce": split_ms[0], "k_yogi_step": split_ms[1],
                                                   "k_reduce_launches": launches - 1}
@@ -1206,9 +1295,17 @@ def main():
         if other is not None:
             res["other_configs"] = other
         if world == 1 and args.cpu_seconds > 0:
-            res["cpu_baseline"] = cpu_baseline(K, P, args.cpu_seconds, args.seed)
+            res["cpu_baseline"] = cpu_baseline(K, P, args.cpu_seconds, args.seed, policy)
         else:
-            res["cpu_baseline"] = None
+            res["cpu_baseline"] = cpu_base
+            if world == 1 or args.cpu_seconds <= 0:
+                res["cpu_legs_off"] = True
+        if world == 1 and other is not None and "headline_model_pcie_inclusive" in other:
+            res["pcie_inclusive"] = dict(other["headline_model_pcie_inclusive"], n_gpus=1)
+        elif pcie is not None:
+            res["pcie_inclusive"] = pcie
+        missing = check_line(res)
+        res["schema"] = {"complete": not missing, "missing": missing}
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.barrier(group=cpu_group)

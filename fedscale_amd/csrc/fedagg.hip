@@ -952,10 +952,23 @@ struct QfArgs {
 // vote per client.  The residual is formed negated, nrem = b*q - a, and the correction is q - nrem*r:
 // the same exact values for a != 0, and the signed zero IEEE gives for a = -0 (b > 0: q = -0,
 // nrem = +0, -0 + -0 = -0), where q + (a - b*q)*r would round -0 + +0 to +0.
+// QF_DIV_MUL 1 (tuning builds only, WRONG BITS): the quotient is a * RN(1/b) with no correction — a power / clock
+// probe of the division's cost at the card's power cap (tools/gpu/r6_div_power.sh), never a product.
+#ifndef QF_DIV_MUL
+#define QF_DIV_MUL 0
+#endif
+#if QF_DIV_MUL && !FA_TUNING
+#error "QF_DIV_MUL changes results: a tuning build only (-DFA_TUNING=1)"
+#endif
 __device__ __forceinline__ float fast_div(float a, float b, float r) {
   const float q = a * r;
+#if QF_DIV_MUL
+  (void)b;
+  return q;
+#else
   const float nrem = __builtin_fmaf(q, b, -a);
   return __builtin_fmaf(-nrem, r, q);
+#endif
 }
 // QF_INFCHK 1: +-inf inputs are caught per element (max |a|).  2: they are caught once per client and
 // lane instead: an infinite a makes the fast quotient NaN (its residual is inf - inf), so the lane's

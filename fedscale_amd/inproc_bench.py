@@ -172,20 +172,154 @@ def run(devices, K: int = 1000, P: int = 25_000_000, rounds: int = 6, warmup: in
             with torch.cuda.device(d):
                 torch.cuda.empty_cache()
     if one_gpu:
-        d0 = devices[0]
-        one = TorchModelAdapter(_model(P, seed), optimizer=_optimizer(policy, d0), device=d0, staging_capacity=K)
+        out["one_gpu"] = run_one(devices[0], K, P, rounds, warmup, seed, policy)
+        out["speedup_vs_one_gpu"] = out["one_gpu"]["round_ms"] / out["inproc_round_ms"]
+        out["speedup_vs_one_gpu_incl_egress"] = (out["one_gpu"]["round_ms_incl_egress"]
+                                                 / out["inproc_round_ms_incl_egress"])
+    return out
+
+
+def run_one(device, K: int = 1000, P: int = 25_000_000, rounds: int = 6, warmup: int = 2, seed: int = 2024,
+            policy: str = "fedavg") -> dict:
+    """The same device-resident round through the single-device ``TorchModelAdapter`` on ``device``: the one-GPU
+    figure of this methodology (the N > 1 line's ``scaling_vs_one_gpu`` divides by it; the N = 1 line reports it as
+    ``value_drop_in``)."""
+    import torch
+
+    from . import synth
+    from .cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    one = TorchModelAdapter(_model(P, seed), optimizer=_optimizer(policy, device), device=device, staging_capacity=K)
+    try:
         rnd = one.begin_round(K, "fedavg", capacity=K)
         with one.dstream:
             synth.fill(rnd.staging.x, K, P, seed=seed)
         r1 = _time_rounds(one, [one.dstream], K, rounds, warmup)
-        out["one_gpu"] = {"device": d0, "round_ms": r1["round_ms"], "kernel_ms": r1["part_kernel_ms"][0],
-                          "client_updates_per_s": K / (r1["round_ms"] * 1e-3), "egress_ms": r1["egress_ms"],
-                          "round_ms_incl_egress": r1["round_ms_incl_egress"]}
-        out["speedup_vs_one_gpu"] = r1["round_ms"] / out["inproc_round_ms"]
-        out["speedup_vs_one_gpu_incl_egress"] = r1["round_ms_incl_egress"] / out["inproc_round_ms_incl_egress"]
-        del one, rnd
-        with torch.cuda.device(d0):
+    finally:
+        del one
+        with torch.cuda.device(device):
             torch.cuda.empty_cache()
+    return {"device": device, "round_ms": r1["round_ms"], "kernel_ms": r1["part_kernel_ms"][0],
+            "client_updates_per_s": K / (r1["round_ms"] * 1e-3), "egress_ms": r1["egress_ms"],
+            "round_ms_incl_egress": r1["round_ms_incl_egress"], "rounds": rounds, "warmup": warmup}
+
+
+# ------------------------------------------------------------------------------------------------
+# the PCIe-inclusive round (SURVEY §8d's second figure): executors' pickled payloads -> host -> N GPUs -> model out
+# ------------------------------------------------------------------------------------------------
+def headline_model(seed: int = 0):
+    """The headline's 25 M-fp32 model as the PCIe-inclusive round ships it: 10 tensors of 2.5 M (100 MB per upload)."""
+    import torch
+
+    from . import synth
+
+    names, shapes = [f"l{i}.weight" for i in range(10)], [(2500, 1000)] * 10
+    return synth.LayoutModule(names, shapes, [torch.float32] * 10, seed=seed)
+
+
+def pcie_rounds(adapter, K: int = 64, rounds: int = 6, seed: int = 2024, n_payloads: int = 8) -> dict:
+    """Rounds of the deployed path from the executors' pickled upload payloads (CLIENT_EXECUTE_COMPLETION,
+    job_api.proto:31-39) to the new global model on the host: the mixin's zero-copy ``deserialize_response``
+    (aggregator.py:704), the adapter's ingress (one GPU: pinned gather + H2D; ``ShardedModelAdapter``: the payload
+    registered in place and every GPU's copy engine reading its slice over its own link), the reduce on every GPU,
+    and ``get_weights()`` (D2H egress, torch_model_adapter.py:41-47).  ``n_payloads`` distinct payloads are reused
+    round robin.  Median and min of ``rounds`` rounds after one warm-up round; synchronised on every GPU."""
+    import pickle
+
+    import numpy as np
+    import torch
+
+    from .cloud.aggregation.aggregator import DeviceAggregator
+
+    model = adapter.model
+    devs = sorted({d.index for d in getattr(getattr(adapter, "group", None), "devices", [adapter.device])})
+    agg = DeviceAggregator(adapter)
+    rng = np.random.default_rng(seed)
+    payloads = []
+    for i in range(n_payloads):
+        up = {n: t.numpy() + rng.standard_normal(t.shape, dtype=np.float32) * np.float32(0.01)
+              for n, t in model.state_dict().items()}
+        payloads.append(pickle.dumps({"client_id": i, "moving_loss": 1.0, "trained_size": 200, "success": True,
+                                      "utility": 1.0, "update_weight": up, "wall_duration": 0}))
+        del up
+
+    def sync():
+        for d in devs:
+            torch.cuda.synchronize(d)
+
+    ts, t_in, t_fin, t_eg = [], [], [], []
+    for r in range(rounds + 1):
+        sync()
+        t0 = time.perf_counter()
+        agg.start_round(K)
+        for k in range(K - 1):
+            agg.on_result(agg.deserialize_response(payloads[k % n_payloads]))
+        t1 = time.perf_counter()
+        agg.on_result(agg.deserialize_response(payloads[(K - 1) % n_payloads]))  # the K-th: its H2D, then the reduce
+        sync()
+        t2 = time.perf_counter()
+        adapter.get_weights()
+        t3 = time.perf_counter()
+        if r:
+            ts.append(t3 - t0)
+            t_in.append(t1 - t0)
+            t_fin.append(t2 - t1)
+            t_eg.append(t3 - t2)
+    s, smin = float(np.median(ts)), float(np.min(ts))
+    tin = float(np.median(t_in))
+    P = adapter.layout.P_full
+    out = {"clients": K, "params": P, "payload_bytes": len(payloads[0]), "round_ms": s * 1e3, "round_ms_min": smin * 1e3,
+           "rounds_ms": [t * 1e3 for t in ts], "client_updates_per_s": K / s, "client_updates_per_s_best": K / smin,
+           "host_to_device_GBps": 4 * K * P / s / 1e9, "host_to_device_GBps_best": 4 * K * P / smin / 1e9,
+           "phases_ms": {"ingress_first_K_minus_1": tin * 1e3, "last_upload_and_reduce": float(np.median(t_fin)) * 1e3,
+                         "egress_get_weights": float(np.median(t_eg)) * 1e3},
+           "ingress_GBps": 4 * (K - 1) * P / tin / 1e9}
+    if hasattr(adapter, "registered_uploads"):
+        out["registered_uploads"] = adapter.registered_uploads
+        out["registration_fallbacks"] = adapter.registration_fallbacks
+    del agg, payloads
+    return out, tin
+
+
+def run_pcie(devices, K: int = 64, rounds: int = 6, seed: int = 2024) -> dict:
+    """The PCIe-inclusive round of the headline model over ``devices``: one GPU through ``TorchModelAdapter``,
+    several through ``ShardedModelAdapter`` (one part per GPU, each fed over its own link).  ``parts``: per GPU its
+    slice, the host NUMA node its link hangs off (sysfs) and the rate its link carried over the ingress phase
+    (its slice's bytes of the K - 1 uploads / that phase's wall: the parts copy concurrently)."""
+    import torch
+
+    from .cloud.internal.sharded_model_adapter import ShardedModelAdapter
+    from .cloud.internal.torch_model_adapter import TorchModelAdapter
+    from .hostnuma import gpu_numa_node
+
+    N = len(devices)
+    model = headline_model()
+    if N == 1:
+        adapter = TorchModelAdapter(model, device=devices[0])
+        parts = [(devices[0], adapter.layout.P_full)]
+    else:
+        adapter = ShardedModelAdapter(model, devices=list(devices))
+        parts = [(p.device.index, p.layout.P) for p in adapter.parts]
+    try:
+        out, tin = pcie_rounds(adapter, K=K, rounds=rounds, seed=seed)
+        out.update({"devices": list(devices), "n_gpus": N, "distinct_gpus": len(set(devices)) == N,
+                    "transport": getattr(getattr(adapter, "group", None), "transport", "single device"),
+                    "adapter": type(adapter).__name__})
+        out["parts"] = [{"device": d, "params": n, "host_numa_node": gpu_numa_node(torch.device("cuda", d)),
+                         "h2d_GBps_over_ingress": 4 * (K - 1) * n / tin / 1e9} for d, n in parts]
+    finally:
+        if hasattr(adapter, "close"):
+            adapter.close()
+        del adapter
+        for d in set(devices):
+            with torch.cuda.device(d):
+                torch.cuda.empty_cache()
+    out["note"] = ("from pickled executor payloads: zero-copy deserialize_response, ingress (one GPU: pinned gather + "
+                   "H2D; N GPUs: the payload registered in place, each GPU's copy engine reading its slice over its own "
+                   "link), reduce, get_weights() D2H; median and min of %d rounds after one warm-up round; never `value`"
+                   % rounds)
+    if not out["distinct_gpus"]:
+        out["note"] += "; %d parts on %d GPU(s): plumbing, not an N-link rate" % (N, len(set(devices)))
     return out
 
 
@@ -199,8 +333,18 @@ def main(argv=None):
     p.add_argument("--warmup", type=int, default=2)
     p.add_argument("--no-one-gpu", action="store_true")
     p.add_argument("--policies", default="fedavg", help="comma-separated: fedavg, fed-yogi")
+    p.add_argument("--pcie", action="store_true", help="the PCIe-inclusive round from pickled payloads (run_pcie) "
+                                                       "instead of the device-resident one; --clients defaults to 64")
     a = p.parse_args(argv)
     devices = [int(d) for d in a.devices.split(",") if d.strip()]
+    if a.pcie:
+        try:
+            rep = run_pcie(devices, K=a.clients if a.clients != 1000 else 64, rounds=a.rounds)
+            rep["ok"] = True
+        except Exception as e:
+            rep = {"devices": devices, "ok": False, "error": f"{type(e).__name__}: {e}"}
+        print(json.dumps(rep), flush=True)
+        return 0 if rep["ok"] else 1
     reps = {}
     for pol in [x.strip() for x in a.policies.split(",") if x.strip()]:
         try:

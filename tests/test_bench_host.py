@@ -122,3 +122,68 @@ def test_promote_inproc_value():
     res2 = {"value": 1.0, "ms_per_step": 2.0, "config": {"parallelism": "x"}}
     bench.promote_inproc(res2, {"ok": False, "policies": {"fedavg": {"ok": False, "error": "boom"}}}, 1000, 20)
     assert res2["value"] == 1.0 and "boom" in res2["value_source"] and "value_spmd" not in res2
+    # parts sharing one card (a gloo rehearsal) are plumbing: the SPMD value stays
+    res3 = {"value": 1.0, "ms_per_step": 2.0, "config": {"parallelism": "x"}}
+    shared = {"ok": True, "inproc_round_ms": 2.5, "devices": [0, 0], "distinct_gpus": False, "transport": "copy"}
+    bench.promote_inproc(res3, shared, 1000, 20)
+    assert res3["value"] == 1.0 and "plumbing" in res3["value_source"] and "value_spmd" not in res3
+
+
+def _line(n_gpus, with_cpu=True, with_pcie=True):
+    res = {"metric": bench.CONFIGS and "m", "value": 1.0, "unit": "client-updates/s", "n_gpus": n_gpus, "steps": 5,
+           "warmup": 2, "ms_per_step": 1.0, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+           "dtype": "f32", "data": "synthetic", "config": {"workload": "w"},
+           "roofline": {"bound": "hbm", "achieved": 1.0, "peak": 8000.0, "unit": "GB/s", "frac": 1 / 8000, "traffic": None},
+           "cpu_baseline": ({"value": 80.0, "unit": "client-updates/s", "cores": 1, "kind": "port", "sample": "s"}
+                            if with_cpu else None)}
+    if with_pcie:
+        res["pcie_inclusive"] = {"ok": True, "round_ms": 100.0, "client_updates_per_s": 640.0,
+                                 "host_to_device_GBps": 64.0, "phases_ms": {}, "prediction": bench.pcie_prediction(n_gpus),
+                                 "parts": [{"device": i, "params": 1, "host_numa_node": 0, "h2d_GBps_over_ingress": 8.0}
+                                           for i in range(n_gpus)]}
+    return res
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_n_gt_1_line_must_carry_cpu_baseline_and_pcie_inclusive(n):
+    """an N > 1 line without the CPU baseline or the PCIe-inclusive N-link round is incomplete (the
+    north star wants both beside the 1/2/4/8-GPU figures)."""
+    assert bench.check_line(_line(n)) == []
+    assert "cpu_baseline (null)" in bench.check_line(_line(n, with_cpu=False))
+    assert "pcie_inclusive" in bench.check_line(_line(n, with_pcie=False))
+    bad = _line(n)
+    bad["pcie_inclusive"]["parts"] = bad["pcie_inclusive"]["parts"][:-1]
+    del bad["pcie_inclusive"]["parts"][0]["host_numa_node"]
+    miss = bench.check_line(bad)
+    assert any("parts (" in m for m in miss) and "pcie_inclusive.parts[0].host_numa_node" in miss
+    failed = _line(n)
+    failed["pcie_inclusive"] = {"ok": False, "error": "boom"}
+    assert any("boom" in m for m in bench.check_line(failed))
+
+
+def test_n1_line_schema():
+    assert bench.check_line(_line(1, with_pcie=False)) == []
+    off = _line(1, with_cpu=False, with_pcie=False)
+    assert bench.check_line(off) == ["cpu_baseline (null)"]
+    off["cpu_legs_off"] = True
+    assert bench.check_line(off) == []
+    broken = _line(1)
+    del broken["roofline"]["traffic"]
+    assert bench.check_line(broken) == ["roofline.traffic"]
+
+
+def test_pcie_prediction_scales_with_links():
+    p1, p8 = bench.pcie_prediction(1), bench.pcie_prediction(8)
+    assert p8["host_to_device_GBps"] == 8 * p1["host_to_device_GBps"] == 8 * bench.PCIE_LINK_GBPS
+
+
+def test_committed_rehearsal_lines_are_complete():
+    """The N > 1 rehearsal lines committed this round (bench.py --gpus 2 / 8 under gloo on one card) carry every
+    north-star quantity (labelled as plumbing)."""
+    import glob
+
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "r06_bench_gloo_rehearsal_*.json")))
+    for p in paths:
+        line = json.loads([ln for ln in open(p).read().splitlines() if ln.startswith("{")][-1])
+        assert line["n_gpus"] > 1 and bench.check_line(line) == [], (p, bench.check_line(line))
+        assert line["schema"]["complete"] and "plumbing" in json.dumps(line["pcie_inclusive"])
