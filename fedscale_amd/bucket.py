@@ -22,6 +22,8 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from . import hoststage
+
 ALIGN = 64  # floats: 256-byte rows, and the shard granule
 
 
@@ -396,6 +398,7 @@ class ClientStaging:
             # small update (config 1: 8 tensors, 98 KB) is validated and copied entry by entry in a few µs
             # instead of building a gather plan and crossing into the native gather
             self._views = [None] * self.capacity if layout.world == 1 else None  # built per slot on first use
+            self._dsts = [None] * self.capacity  # the views alone (hoststage.stage's destinations)
 
     def _copy_in(self, slot, plan, r, stream, on_current: bool):
         """Gather into ring entry r's pinned rows, then enqueue their H2D on ``stream`` and record r's event
@@ -520,8 +523,10 @@ class ClientStaging:
 
     def _put_bulk_views(self, slot: int, values) -> bool:
         """Small whole-model update of plain numpy arrays: validate (shape, dtype) and copy each entry into
-        its pinned view.  False (nothing written) when an entry is not a plain ndarray: the general path
-        converts and reports it."""
+        its pinned view — in one native call (fedscale_amd/csrc/hoststage.c), which stops at the first entry it
+        does not take (not a plain C-contiguous array of the entry's shape and dtype) and leaves it and the rest
+        to the loop below.  False when an entry is not a plain ndarray: the general path converts and reports it
+        (and rewrites every entry of the slot)."""
         views = self._views[slot]
         if views is None:
             views = self._views[slot] = [
@@ -529,13 +534,19 @@ class ClientStaging:
                  (self._hx_np[slot, e.offset:e.offset + e.numel] if e.kind == "f" else
                   self._hxi_np[slot, e.offset:e.offset + e.numel]).reshape(e.shape))
                 for e in self.layout.entries]
-        for a in values:
-            if type(a) is not np.ndarray:
-                return False
+            self._dsts[slot] = [v[3] for v in views]
+        if type(values) is not list:
+            values = list(values)
         self._claim_bulk(slot)
         # validated entry by entry as it is copied: an error leaves the slot uncommitted (_bulk_hi is not
         # advanced), so the next update written to it overwrites every entry
-        for (name, shape, dt, dst), a in zip(views, values):
+        i = hoststage.stage(values, self._dsts[slot])
+        if i < 0:
+            self._bulk_hi = slot + 1
+            return True
+        for (name, shape, dt, dst), a in zip(views[i:], values[i:]):
+            if type(a) is not np.ndarray:
+                return False
             if a.shape != shape:
                 raise ValueError(f"{name}: shape {tuple(a.shape)} != model shape {shape}")
             if a.dtype != dt:

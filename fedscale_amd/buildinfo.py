@@ -81,6 +81,54 @@ def build(out: str = LIB, defs: str = "", force: bool = False) -> bool:
     return True
 
 
+# ---- the host staging extension (fedscale_amd/_hoststage: CPython C API, gcc) ------------------------------------
+HOST_SRC = "fedscale_amd/csrc/hoststage.c"
+HOST_FLAGS = ("-O2", "-shared", "-fPIC", "-Wall", "-Werror", "-std=c11")
+
+
+def host_module_path() -> str:
+    import sysconfig
+
+    return os.path.join(ROOT, "fedscale_amd", "_hoststage" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def host_source_id(root: str = ROOT) -> str:
+    """Build id of the host staging extension: SHA-256 over its flags and source (as ``source_id`` does for the
+    HIP library)."""
+    h = hashlib.sha256()
+    h.update(" ".join(HOST_FLAGS).encode() + b"\0")
+    with open(os.path.join(root, HOST_SRC), "rb") as f:
+        data = f.read()
+    h.update(HOST_SRC.encode() + b"\0" + str(len(data)).encode() + b"\0" + data)
+    return h.hexdigest()[:16]
+
+
+def build_host(out: str = None, force: bool = False) -> bool:
+    """Compile the host staging extension unless it already carries the source's id; True when it compiled."""
+    import sysconfig
+
+    import numpy as np
+
+    out = out or host_module_path()
+    want = host_source_id()
+    if not force and embedded_id(out) == want:
+        return False
+    tmp = out + ".tmp%d" % os.getpid()
+    cmd = ([os.environ.get("CC", "gcc")] + list(HOST_FLAGS) +
+           ["-I" + sysconfig.get_paths()["include"], "-I" + np.get_include(),
+            f"-DHS_BUILD_ID=\"FA_BUILD_ID={want}\"", "-o", tmp, os.path.join(ROOT, HOST_SRC)])
+    print("[build]", " ".join(cmd), flush=True)
+    try:
+        subprocess.run(cmd, check=True, cwd="/tmp")
+        if embedded_id(tmp) != want:
+            raise RuntimeError(f"{tmp}: the build does not carry the id {want}")
+        os.replace(tmp, out)
+    finally:
+        if os.path.exists(tmp):
+            os.unlink(tmp)
+    return True
+
+
 def main(argv=None) -> int:
     import argparse
 

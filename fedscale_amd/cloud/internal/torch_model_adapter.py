@@ -26,6 +26,7 @@ import torch
 
 from ...bucket import BucketLayout, ClientStaging
 from ... import kernels as kx
+from ..._native import FA_FINALIZE, FedAggError
 from ...kernels import qfed_max_chunk as kx_qfed_max_chunk
 from ...round import DeviceRound, default_capacity
 from ...state import DeviceStream, FlatState, ShardGroup
@@ -191,6 +192,7 @@ class TorchModelAdapter(ModelAdapterBase):
         model into (fa_reduce_mirror); it becomes the new version's egress snapshot, so egress needs no D2H."""
         self._ready_stream = self.dstream.stream  # every write to the model buffers is issued on it
         self._ready.record(self._ready_stream)
+        self._commit_ev = self._ready
         with self._egress_lock:  # (buffer, version) flip atomically for the servicer threads
             self._cur = 1 - self._cur
             self._version += 1
@@ -456,8 +458,15 @@ class TorchModelAdapter(ModelAdapterBase):
     def apply_round(self, rnd: DeviceRound, denom32: float, denom64: float, client_training_results=None,
                     keep_mean: bool = True):
         """Finish a round: reduce the last chunk with the server step fused, then swap buffers."""
-        with self.dstream.joined():
+        self._commit_ev = None
+        with self.dstream.joined(self._take_commit_event):
             self._apply_round(rnd, denom32, denom64, keep_mean)
+
+    def _take_commit_event(self):
+        """The event ``_commit_scratch`` recorded for the round just applied (after all of its work on the
+        dstream): the caller's stream waits on it instead of a second record (DeviceStream.joined)."""
+        ev, self._commit_ev = getattr(self, "_commit_ev", None), None
+        return ev
 
     def _apply_round(self, rnd: DeviceRound, denom32: float, denom64: float, keep_mean):
         L = self.layout
@@ -494,13 +503,60 @@ class TorchModelAdapter(ModelAdapterBase):
             raise RuntimeError("q-fedavg optimizer but the round was not staged as q-FedAvg")
         else:
             host = self._mirror_target()
-            rnd.finalize_mean(denom32, denom64, out=out_f, cur_side=self._mean_s, model_side=out_s,
-                              mirror=None if host is None else host.f)
+            if not self._finish_small(rnd, denom32, out_f, host):
+                rnd.finalize_mean(denom32, denom64, out=out_f, cur_side=self._mean_s, model_side=out_s,
+                                  mirror=None if host is None else host.f)
             self._mean_f = out_f  # FedAvg without a server step: the mean IS the new model
             self._mean_valid = True
             self._commit_scratch(host)
             return
         self._commit_scratch()
+
+    #: the small-round finish (``_finish_small``); False takes DeviceRound.finalize_mean for every round
+    SMALL_ROUND_FINISH = True
+
+    def _finish_small(self, rnd: DeviceRound, denom32: float, out_f: torch.Tensor, host) -> bool:
+        """FedAvg's finishing reduce for a small single-chunk round whose updates are all still in the staging's
+        pinned mirror and whose model has no int64 entries (config 1, the FEMNIST CNN): the one fa_reduce_mirror
+        launch DeviceRound.finalize_mean would make (x read over PCIe from the mirror, the mean written to the new
+        model buffer and to its egress snapshot), issued straight through the C ABI.  The same launch on the same
+        stream, so the same bits; the host cost of the general path's argument checks (which the ABI repeats on
+        every operand, fa_device.h) is paid once per (rows, model buffer, snapshot) triple and cached.  False:
+        the round does not qualify (the caller takes finalize_mean)."""
+        L = self.layout
+        if (not self.SMALL_ROUND_FINISH or host is None or L.Q or rnd.policy != "fedavg" or rnd.chunks_done
+                or rnd.cg is not None):
+            return False
+        rnd._check_complete()
+        st = rnd.staging
+        n = rnd.slot
+        zc = st.host_rows(n)
+        if zc is None:
+            return False
+        x = zc[0]
+        key = (x.data_ptr(), n, out_f.data_ptr(), host.f.data_ptr())
+        cache = self.__dict__.setdefault("_small_keys", set())
+        if key not in cache:  # the wrapper's checks, once per triple (kernels.reduce_mirror)
+            kx._check_x(x, n, L.P, host_ok=True)
+            kx._dev(out_f, torch.float32, "out", kx._cols(L.P))
+            kx._pinned(host.f, torch.float32, "mirror", kx._cols(L.P))
+            if len(cache) > 64:
+                cache.clear()
+            cache.add(key)
+        try:
+            rc = self._lib.fa_reduce_mirror(key[0], x.shape[1], n, L.P, None, None, key[2], key[3], denom32,
+                                            FA_FINALIZE, self.dstream.handle)
+        finally:
+            st.release_host_rows()  # the mirror's rows are rewritten only after the stream has passed the reads
+        if rc:
+            raise FedAggError("fa_reduce_mirror failed (%d): %s" % (rc, self._lib.fa_last_error_string().decode()))
+        return True
+
+    @property
+    def _lib(self):
+        from ... import _native
+
+        return _native.load()
 
     def _finish_qfed(self, rnd: DeviceRound):
         """hs + step of a folded q-FedAvg round (its norms already summed over the shards), then commit."""

@@ -133,25 +133,30 @@ class DeviceStream:
     def __exit__(self, *exc):
         return self._exit(False)
 
-    def _exit(self, join: bool):
+    def _exit(self, join: bool, done=None):
         _, prev_dev, prev = self._tls.stack.pop()
         if join and prev != self.key:  # no host sync: the caller's stream is ordered after our work
-            ev = self._join_ev
+            # ``done()``: an event the body has ALREADY recorded on this stream after all of its work (an adapter's
+            # commit event), or None — then one is recorded here
+            ev = done() if done is not None else None
             if ev is None:
-                ev = self._join_ev = torch.cuda.Event()
-            ev.record(self.stream)
+                ev = self._join_ev
+                if ev is None:
+                    ev = self._join_ev = torch.cuda.Event()
+                ev.record(self.stream)
             _stream_obj(prev).wait_event(ev)
         _set_stream(prev)
         if prev_dev != self.index:
             _set_device(prev_dev)
         return False
 
-    def joined(self) -> "_Joined":
+    def joined(self, done=None) -> "_Joined":
         """Like ``with ds:``, and on exit the caller's stream on this device waits for everything issued
         inside (an event, no host sync): an adapter's public calls keep the ordering a caller on its own
         stream expects (device buffers it reads afterwards are written), while the work itself runs on
-        ``stream``."""
-        return _Joined(self)
+        ``stream``.  ``done``: a callable returning an event the body recorded on ``stream`` after ALL of its
+        work (or None), which the caller's stream then waits on instead of a fresh record."""
+        return _Joined(self, done)
 
     def wait_caller(self):
         """Order this stream after the work the caller queued on this device before its outermost entry."""
@@ -166,16 +171,16 @@ class DeviceStream:
 
 
 class _Joined:
-    __slots__ = ("ds",)
+    __slots__ = ("ds", "done")
 
-    def __init__(self, ds: DeviceStream):
-        self.ds = ds
+    def __init__(self, ds: DeviceStream, done=None):
+        self.ds, self.done = ds, done
 
     def __enter__(self):
         return self.ds.__enter__()
 
     def __exit__(self, *exc):
-        return self.ds._exit(True)
+        return self.ds._exit(True, None if exc[0] is not None else self.done)
 
 
 @dataclass

@@ -21,8 +21,12 @@ def _ensure_library():
     without hipcc a missing library fails the tests loudly."""
     import __graft_entry__ as entry
 
-    if not os.path.exists(entry.LIB) and (os.path.exists(entry.HIPCC) or shutil.which("hipcc")):
+    if not os.path.exists(entry.LIB) and (os.path.exists("/opt/rocm/bin/hipcc") or shutil.which("hipcc")):
         entry.build()
+    from fedscale_amd import buildinfo
+
+    if not os.path.exists(buildinfo.host_module_path()) and shutil.which("gcc"):
+        buildinfo.build_host()
 
 
 @pytest.fixture(scope="session")
