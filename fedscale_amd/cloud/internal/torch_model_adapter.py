@@ -26,7 +26,7 @@ import torch
 
 from ...bucket import BucketLayout, ClientStaging
 from ... import kernels as kx
-from ..._native import FA_FINALIZE, FedAggError
+from ..._native import FA_FINALIZE
 from ...kernels import qfed_max_chunk as kx_qfed_max_chunk
 from ...round import DeviceRound, default_capacity
 from ...state import DeviceStream, FlatState, ShardGroup
@@ -544,19 +544,11 @@ class TorchModelAdapter(ModelAdapterBase):
                 cache.clear()
             cache.add(key)
         try:
-            rc = self._lib.fa_reduce_mirror(key[0], x.shape[1], n, L.P, None, None, key[2], key[3], denom32,
-                                            FA_FINALIZE, self.dstream.handle)
+            kx.call("fa_reduce_mirror", key[0], x.shape[1], n, L.P, None, None, key[2], key[3], denom32, FA_FINALIZE,
+                    self.dstream.handle)
         finally:
             st.release_host_rows()  # the mirror's rows are rewritten only after the stream has passed the reads
-        if rc:
-            raise FedAggError("fa_reduce_mirror failed (%d): %s" % (rc, self._lib.fa_last_error_string().decode()))
         return True
-
-    @property
-    def _lib(self):
-        from ... import _native
-
-        return _native.load()
 
     def _finish_qfed(self, rnd: DeviceRound):
         """hs + step of a folded q-FedAvg round (its norms already summed over the shards), then commit."""

@@ -18,3 +18,6 @@ print("c1", o["c1_femnist_cnn_k10_host_round"]["round_ms_incl_h2d_d2h"], o["c1_f
 print("c5 chain", o["c5_qfedavg_k10000_p100M"]["round_ms"], o["c5_qfedavg_k10000_p100M"].get("no_chain", {}).get("chain_cost_pct"))
 print("drop_in", l.get("value_drop_in"), "pcie", l["pcie_inclusive"]["host_to_device_GBps"])
 PY
+timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 8 --steps 5 --warmup 2 --dist-backend gloo --mem-fraction 0.06 --cpu-seconds 3 > $O/r6b_rehearse_8.log 2>&1 || { tail -40 $O/r6b_rehearse_8.log; exit 1; }
+grep '^{' $O/r6b_rehearse_8.log > $O/r6_bench_gloo_rehearsal_8.json
+echo rehearsal8 ok
