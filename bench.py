@@ -594,7 +594,7 @@ def pmc_traffic(workload: str, resident: int, launches: int, build_id: str, path
 #: of the line, takes no rest unless --rest is given).  100 s of back-to-back headline rounds showed no decay
 #: (profiles/r05_sustain100.json), but the configs timed one after another do: without a rest config 5 on one GPU ran
 #: at the board's 1400 W cap (1384 W mean) with the shader clock down to 2150 MHz, and the shard of 8 timed after it at
-#: 1810 MHz, 3 % slower (profiles/r05_bench_default_n1_norest.json).  An aggregator's GPU works in bursts (one round,
+#: 1810 MHz, 3 % slower (a round-5 no-rest line).  An aggregator's GPU works in bursts (one round,
 #: then idle while the clients train), so each config is timed from a rested card and ALSO back to back right after
 #: (``sustained`` on each config line), both with the card's telemetry.  Outside the timed region.
 REST_S = 12.0
@@ -903,8 +903,8 @@ def run_inproc_bench(world: int, K: int, P: int, backend: str, steps: int = 6, w
     return rep
 
 
-#: one PCIe link's rate for the PCIe-inclusive round of the headline model on one GPU (profiles/r05_bench_default_n1_final.json
-#: headline_model_pcie_inclusive: 52-54 GB/s end to end, the copy engine's 56-57 GB/s, r01_h2d_probe.json): the
+#: one PCIe link's rate for the PCIe-inclusive round of the headline model on one GPU (BENCH_r05.json
+#: other_configs.headline_model_pcie_inclusive: 53.8 GB/s end to end, the copy engine's 56-57 GB/s, r01_h2d_probe.json): the
 #: basis of the N-link prediction each N > 1 line carries
 PCIE_LINK_GBPS = 54.0
 

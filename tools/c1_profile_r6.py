@@ -80,6 +80,18 @@ def main():
     agg, K, ups = make(dev)
     rows = run_rounds(agg, K, ups)
     print(json.dumps({"round_unwrapped_us": med(rows, "round")}), flush=True)
+    # the drop-in's round with each knob off in turn (A/B of this round's changes), interleaved
+    knobs = {"all_on": {}, "small_finish_off": {"SMALL_ROUND_FINISH": False}, "spin_200us": {"EGRESS_SPIN_S": 2e-4}}
+    res = {k: [] for k in knobs}
+    aggs = {k: make(dev) for k in knobs}
+    for rep in range(6):
+        for k, kv in knobs.items():
+            a, KK, u = aggs[k]
+            for attr, v in kv.items():
+                setattr(a.model_wrapper, attr, v)
+            rows = run_rounds(a, KK, u, n=100, warm=10)
+            res[k].append(med(rows, "round"))
+    print(json.dumps({"ab_round_us": {k: sorted(v) for k, v in res.items()}}), flush=True)
     wraps = [(bucket.ClientStaging, "put"), (bucket.ClientStaging, "_put_bulk_views"),
              (bucket.ClientStaging, "_claim_bulk"), (bucket.ClientStaging, "host_rows"),
              (bucket.ClientStaging, "release_host_rows"), (rd.DeviceRound, "add"), (rd.DeviceRound, "finalize_mean"),
@@ -136,6 +148,32 @@ def main():
             fl["clones"].append(t5 - t4)
         del cl
     print(json.dumps({"floors_us": {k: round(float(np.median(v)) * 1e6, 2) for k, v in fl.items()}}), flush=True)
+    # how the host waits: event synchronize against spinning on event.query(), and the kernel's own time by events
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    w = {"record_sync": [], "record_spin_query": [], "stream_sync": [], "kernel_by_events_us": []}
+    for r in range(320):
+        for mode in ("record_sync", "record_spin_query", "stream_sync"):
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            if mode == "record_sync":
+                e0.record()
+            lib.fa_reduce_mirror(hx.data_ptr(), L.ld, K, L.P, None, None, outd.data_ptr(), mir.data_ptr(), denom,
+                                 _native.FA_FINALIZE, st)
+            if mode == "stream_sync":
+                torch.cuda.current_stream(dev).synchronize()
+            else:
+                (e1 if mode == "record_sync" else ev).record()
+                if mode == "record_sync":
+                    e1.synchronize()
+                else:
+                    while not ev.query():
+                        pass
+            t2 = time.perf_counter()
+            if r >= 20:
+                w[mode].append(t2 - t1)
+                if mode == "record_sync":
+                    w["kernel_by_events_us"].append(e0.elapsed_time(e1) * 1e-3)
+    print(json.dumps({"wait_us": {k: round(float(np.median(v)) * 1e6, 2) for k, v in w.items()}}), flush=True)
 
 
 if __name__ == "__main__":

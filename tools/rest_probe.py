@@ -2,7 +2,7 @@
 11,191,242 FedAvg) on one GPU: per-round HIP-event times of 10 rounds after each of
   fill+0 s, fill+2 s, fill+12 s, idle 12 s without a fill, and straight after 3 s of back-to-back rounds,
 with the card's telemetry for each region.  bench.py's no-rest line read configs 3-5 about 3 % slower than its
-rested line (profiles/r05_bench_default_n1_norest.json against r05_bench_default_n1_final.json)."""
+rested line (two round-5 lines, since folded into DESIGN.md §5)."""
 import json
 import os
 import sys
