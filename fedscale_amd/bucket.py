@@ -387,6 +387,7 @@ class ClientStaging:
         self.bulk = (not async_ingress and nbytes <= self.BULK_MAX_BYTES) if bulk is None else bool(bulk)
         if self.bulk and async_ingress:
             raise ValueError("bulk staging and async_ingress are exclusive")
+        self._views = None
         if self.bulk:
             self._hx = torch.zeros(self.capacity, layout.ld, dtype=torch.float32).pin_memory()
             self._hxi = torch.zeros(self.capacity, layout.ldq, dtype=torch.int64).pin_memory()
@@ -399,6 +400,7 @@ class ClientStaging:
             # instead of building a gather plan and crossing into the native gather
             self._views = [None] * self.capacity if layout.world == 1 else None  # built per slot on first use
             self._dsts = [None] * self.capacity  # the views alone (hoststage.stage's destinations)
+            self._stage = hoststage.load().stage  # the native call itself (no Python wrapper per upload)
 
     def _copy_in(self, slot, plan, r, stream, on_current: bool):
         """Gather into ring entry r's pinned rows, then enqueue their H2D on ``stream`` and record r's event
@@ -419,6 +421,10 @@ class ClientStaging:
         return ev
 
     def put(self, slot: int, update):
+        if self._views is not None and type(update) is dict:  # a small whole-model upload (config 1): the common case
+            values = list(update.values())
+            if len(values) == self.layout.T and self._put_bulk_views(slot, values):
+                return
         if type(update) is HostRow:
             return self._put_row(slot, update)
         if type(update) is RegisteredUpload:
@@ -537,10 +543,11 @@ class ClientStaging:
             self._dsts[slot] = [v[3] for v in views]
         if type(values) is not list:
             values = list(values)
-        self._claim_bulk(slot)
+        if self._bulk_busy or self._bulk_hi != slot or slot == self._bulk_lo:
+            self._claim_bulk(slot)  # (the steady state — the next contiguous slot, the mirror idle — needs none)
         # validated entry by entry as it is copied: an error leaves the slot uncommitted (_bulk_hi is not
         # advanced), so the next update written to it overwrites every entry
-        i = hoststage.stage(values, self._dsts[slot])
+        i = self._stage(values, self._dsts[slot])
         if i < 0:
             self._bulk_hi = slot + 1
             return True

@@ -262,13 +262,14 @@ class DeviceAggregatorMixin:
         return sup(request, context)
 
     def update_weight_aggregation(self, results):
-        w = self._wrapper()
-        if self._is_first_result_in_round() or self._device_round is None:
-            self._device_round = w.begin_round(self.tasks_round, self._device_policy(),
-                                               capacity=self.device_round_capacity, keep_mean=self.device_keep_mean)
         rnd = self._device_round
+        if rnd is None or self._is_first_result_in_round():
+            w = self._wrapper()
+            rnd = self._device_round = w.begin_round(self.tasks_round, self._device_policy(),
+                                                     capacity=self.device_round_capacity,
+                                                     keep_mean=self.device_keep_mean)
         if rnd.policy == "qfedavg":
-            a = w.optimizer.args  # optimizers.py:69 reads the live args at step time
+            a = self._wrapper().optimizer.args  # optimizers.py:69 reads the live args at step time
             rnd.add(results["update_weight"], loss=results["moving_loss"], learning_rate=a.learning_rate,
                     q=a.qfed_q)
             if self.device_release_uploads:
@@ -276,6 +277,7 @@ class DeviceAggregatorMixin:
         else:
             rnd.add(results["update_weight"])
         if self._is_last_result_in_round():
+            w = self._wrapper()
             K = self.tasks_round
             # np.divide(w, K): fp32 entries divide by fp32(K), int64 sums by float64(K)
             w.apply_round(rnd, float(np.float32(K)), float(K),

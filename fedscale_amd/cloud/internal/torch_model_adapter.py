@@ -479,7 +479,6 @@ class TorchModelAdapter(ModelAdapterBase):
 
     def _apply_round(self, rnd: DeviceRound, denom32: float, denom64: float, keep_mean):
         L = self.layout
-        last = self._snapshot()
         out_f, out_s = self._scratch_buffers()
         opt = self.optimizer
         mode = getattr(opt, "mode", None) if opt is not None else None
@@ -498,6 +497,7 @@ class TorchModelAdapter(ModelAdapterBase):
             # epilogue (fa_reduce_yogi), 1 % faster at 1000 x 25 M — the fused epilogue's last/m/v traffic sits
             # at the end of every tile with one wave per SIMD to hide it (tools/yogi_ab.py,
             # profiles/r03_yogi_fused_vs_unfused.log)
+            last = self._snapshot()
             y = opt.gradient_controller
             y.bind(L, self.device)
             if self._mean_f is None or self._mean_f is last.f32 or self._mean_f is out_f:

@@ -92,6 +92,15 @@ def main():
             rows = run_rounds(a, KK, u, n=100, warm=10)
             res[k].append(med(rows, "round"))
     print(json.dumps({"ab_round_us": {k: sorted(v) for k, v in res.items()}}), flush=True)
+    # as bench.py runs it: the main thread bound to the GPU's NUMA node (hostnuma.bind_to_gpu), and bench's own round
+    from fedscale_amd.hostnuma import bind_to_gpu
+
+    node = bind_to_gpu(dev)
+    a, KK, u = make(dev)
+    rows = run_rounds(a, KK, u)
+    c1 = bench.c1_host_round(dev, 1)
+    print(json.dumps({"numa_bound": {"node": node, "round_us": med(rows, "round"),
+                                     "bench_c1_host_round_us": c1["round_ms_incl_h2d_d2h"] * 1e3}}), flush=True)
     wraps = [(bucket.ClientStaging, "put"), (bucket.ClientStaging, "_put_bulk_views"),
              (bucket.ClientStaging, "_claim_bulk"), (bucket.ClientStaging, "host_rows"),
              (bucket.ClientStaging, "release_host_rows"), (rd.DeviceRound, "add"), (rd.DeviceRound, "finalize_mean"),
