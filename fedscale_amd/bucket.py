@@ -401,6 +401,8 @@ class ClientStaging:
             self._views = [None] * self.capacity if layout.world == 1 else None  # built per slot on first use
             self._dsts = [None] * self.capacity  # the views alone (hoststage.stage's destinations)
             self._stage = hoststage.load().stage  # the native call itself (no Python wrapper per upload)
+            self.head_acc = None  # DeviceRound._launch_head's running chain (one per staging, reused)
+            self._head_key = None
 
     def _copy_in(self, slot, plan, r, stream, on_current: bool):
         """Gather into ring entry r's pinned rows, then enqueue their H2D on ``stream`` and record r's event

@@ -27,7 +27,7 @@ import torch
 
 from ...bucket import BucketLayout, ClientStaging
 from ... import kernels as kx
-from ..._native import FA_FINALIZE
+from ..._native import FA_ACCUMULATE, FA_FINALIZE
 from ...kernels import qfed_max_chunk as kx_qfed_max_chunk
 from ...round import DeviceRound, default_capacity
 from ...state import DeviceStream, FlatState, ShardGroup
@@ -543,18 +543,23 @@ class TorchModelAdapter(ModelAdapterBase):
         if zc is None:
             return False
         x = zc[0]
-        key = (x.data_ptr(), n, out_f.data_ptr(), host.f.data_ptr())
+        h = rnd.head  # rows [0, h) already reduced into rnd.head_acc (DeviceRound._launch_head)
+        acc = rnd.head_acc if h else None
+        key = (x.data_ptr(), n, h, out_f.data_ptr(), host.f.data_ptr(), acc.data_ptr() if h else 0)
         cache = self.__dict__.setdefault("_small_keys", set())
-        if key not in cache:  # the wrapper's checks, once per triple (kernels.reduce_mirror)
+        if key not in cache:  # the wrapper's checks, once per operand set (kernels.reduce_mirror)
             kx._check_x(x, n, L.P, host_ok=True)
             kx._dev(out_f, torch.float32, "out", kx._cols(L.P))
             kx._pinned(host.f, torch.float32, "mirror", kx._cols(L.P))
+            if h:
+                kx._dev(acc, torch.float32, "acc_in", kx._cols(L.P))
             if len(cache) > 64:
                 cache.clear()
             cache.add(key)
+        flags = FA_FINALIZE | (FA_ACCUMULATE if h else 0)
         try:
-            kx.call("fa_reduce_mirror", key[0], x.shape[1], n, L.P, None, None, key[2], key[3], denom32, FA_FINALIZE,
-                    self.dstream.handle)
+            kx.call("fa_reduce_mirror", key[0] + h * x.shape[1] * 4, x.shape[1], n - h, L.P, None, key[5] or None,
+                    key[3], key[4], denom32, flags, self.dstream.handle)
         finally:
             st.release_host_rows()  # the mirror's rows are rewritten only after the stream has passed the reads
         return True

@@ -136,6 +136,47 @@ class DeviceRound:
         if policy == "qfedavg" and mean_chain and self.cg is None:
             with self._on():
                 self.chain = torch.zeros(L.ld, dtype=torch.float32, device=dev)
+        self.head = 0  # arrivals [0, head) already reduced into head_acc by the head launch (_launch_head)
+        self.head_acc = None
+        self._split_at = self._head_split()
+
+    #: small zero-copy FedAvg rounds (config 1) reduce their first half while the second half is still arriving
+    #: (``_launch_head``); False: one finishing launch over every row
+    SPLIT_SMALL_ROUNDS = True
+
+    def _head_split(self):
+        """The arrival count after which the head launch goes out (None: this round takes no head launch): FedAvg
+        rounds of K >= 4 that fit one chunk of a zero-copy staging mirror (ClientStaging.host_rows: its kernels read
+        the pinned rows over PCIe), on the adapter's own stream, with no int64 entries."""
+        st, L = self.staging, self.layout
+        if (not self.SPLIT_SMALL_ROUNDS or self.policy != "fedavg" or self.cg is not None or self.K < 4
+                or self.cap < self.K or self.dstream is None or L.Q or not st.bulk or st._views is None
+                or self.K * (L.ld * 4 + L.ldq * 8) > st.ZERO_COPY_MAX_BYTES):
+            return None
+        return self.K // 2
+
+    def _launch_head(self):
+        """Reduce the arrivals staged so far, [0, slot), straight out of the pinned mirror into ``head_acc`` (the
+        raw fp32 chain, not divided), on the round's stream: the GPU reads these rows over PCIe while the host
+        stages the rest, and the finishing launch continues the same per-element chain from ``head_acc`` over the
+        remaining rows (aggregator.py:500-503 in arrival order; the bits of one launch over all rows).  The rows are
+        not rewritten before the round's finishing launch has run (release_host_rows)."""
+        st, L, n = self.staging, self.layout, self.slot
+        zc = st.host_rows(n)
+        if zc is None:
+            return
+        acc = st.head_acc
+        if acc is None:
+            with self._on():
+                acc = st.head_acc = torch.empty(L.ld, dtype=torch.float32, device=self.device)
+        x = zc[0]
+        key = (x.data_ptr(), n, acc.data_ptr())
+        if st._head_key != key:  # the wrapper's checks, once per (rows, count, accumulator)
+            kx._check_x(x, n, L.P, host_ok=True)
+            kx._dev(acc, torch.float32, "out", kx._cols(L.P))
+            st._head_key = key
+        kx.call("fa_reduce", key[0], x.shape[1], n, L.P, None, None, key[2], 1.0, 0, self.dstream.handle)
+        self.head, self.head_acc = n, acc
 
     def _init_qfed(self, L, dev):
         self.delta = torch.zeros(L.ld, dtype=torch.float32, device=dev)
@@ -170,6 +211,8 @@ class DeviceRound:
         self.slot += 1
         self.n += 1
         self.n_local += 1
+        if self.slot == self._split_at:
+            self._launch_head()
 
     def adopt_resident(self, n: int):
         """Bench hook (FedAvg): take ``n`` arrivals whose updates are ALREADY in the staging slots
@@ -288,6 +331,8 @@ class DeviceRound:
         if self.policy == "fedbuff":
             a32, a64 = self._chunk_weights()
         acc_in = None if first else self.acc
+        if self.head:  # the head launch reduced rows [0, head): continue its chain over the rest (FedAvg, Q == 0)
+            x, n, acc_in = x[self.head:], n - self.head, self.head_acc
         mode = 0 if self.policy == "fedavg" else 1
         try:
             if yogi is not None:

@@ -116,8 +116,14 @@ def test_config1_rounds_read_the_mirror_and_write_egress(gpu_device, monkeypatch
         for k, u in enumerate(ups):
             agg.on_result({"client_id": k, "update_weight": u, "moving_loss": 1.0})
         mir = [c for c in calls if c[0] == "fa_reduce_mirror"]
-        assert len(mir) == 1 and not [c for c in calls if c[0] == "fa_reduce"], [c[0] for c in calls]
-        assert mir[0][1][0] == adapter.staging._hx.data_ptr(), "the reduce did not read the pinned mirror"
+        head = [c for c in calls if c[0] == "fa_reduce"]
+        assert len(mir) == 1 and len(head) == 1, [c[0] for c in calls]
+        # round 6: the first 5 arrivals are reduced out of the mirror while the last 5 arrive (DeviceRound
+        # _launch_head: raw chain, no finalize), the finishing launch continues the chain over rows 5..9
+        hx, ld = adapter.staging._hx, adapter.staging._hx.shape[1]
+        assert head[0][1][0] == hx.data_ptr() and head[0][1][2] == 5 and head[0][1][8] == 0
+        assert mir[0][1][0] == hx.data_ptr() + 5 * ld * 4, "the reduce did not read the pinned mirror"
+        assert mir[0][1][2] == 5 and mir[0][1][5] == head[0][1][6], "the finish does not continue the head's chain"
         assert mir[0][1][7] == adapter._snap.buf.f.data_ptr(), "the mean was not written into the snapshot"
         want = _oracle_round(ups)
         assert_state_equal(adapter.get_weights(), want, f"round {r}")
@@ -207,3 +213,29 @@ def test_pointer_kinds_and_pageable_rejection(gpu_device):
     assert lib.fa_pointer_kind(pinned.data_ptr() + 64) == 1  # inside the allocation
     assert lib.fa_pointer_kind(pageable.ctypes.data) == -1
     assert lib.fa_pointer_kind(torch.zeros(64).data_ptr()) == -1
+
+
+@pytest.mark.parametrize("K", [1, 3, 4, 5, 7, 10, 16])
+def test_head_launch_keeps_every_bit(gpu_device, monkeypatch, K):
+    """Round 6: small zero-copy FedAvg rounds reduce their first K // 2 arrivals while the rest arrive
+    (DeviceRound._launch_head) and finish with the chain continued from that partial sum; the model is the oracle's,
+    bit for bit, and the same as with one finishing launch over all rows, for every K (K < 4: no head launch)."""
+    from fedscale_amd.round import DeviceRound
+
+    got = {}
+    for split in (True, False):
+        monkeypatch.setattr(DeviceRound, "SPLIT_SMALL_ROUNDS", split)
+        names, tensors, adapter, agg = _femnist_adapter(gpu_device)
+        for r in range(3):
+            ups = _uploads(names, tensors, K, 100 * K + r)
+            agg.start_round(K)
+            for k, u in enumerate(ups):
+                agg.on_result({"client_id": k, "update_weight": u, "moving_loss": 1.0})
+            rnd_head = adapter.staging.head_acc is not None
+            w = adapter.get_weights()
+            assert_state_equal(w, _oracle_round(ups), f"K={K} split={split} round {r}")
+            got[(split, r)] = [t.clone() for t in w]
+        assert rnd_head == (split and K >= 4)
+    for r in range(3):
+        for a, b in zip(got[(True, r)], got[(False, r)]):
+            assert torch.equal(a, b)
