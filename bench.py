@@ -1157,7 +1157,9 @@ def main():
         from fedscale_amd.inproc_bench import run_one
 
         try:
-            drop_in = run_one(local_dev, K, P, rounds=args.steps, warmup=max(2, min(warmup_used, 8)), seed=args.seed)
+            # (at least 30 warmup rounds: with 8 the adapter's rounds read ~3 % slow on a card still ramping its clocks,
+            # while 4 x 20 interleaved rounds of both paths read the same, profiles/r06_dropin_vs_workload.log)
+            drop_in = run_one(local_dev, K, P, rounds=args.steps, warmup=max(30, warmup_used), seed=args.seed)
         except Exception as e:  # reported, never fatal
             drop_in = {"error": f"{type(e).__name__}: {e}"}
 
