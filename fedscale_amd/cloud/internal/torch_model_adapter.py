@@ -19,7 +19,6 @@ from __future__ import annotations
 
 import itertools
 import threading
-import time
 from typing import List, Optional
 
 import numpy as np
@@ -292,10 +291,6 @@ class TorchModelAdapter(ModelAdapterBase):
         if wait is not None:
             # the kernel of THIS version wrote the snapshot (fa_reduce_mirror): wait for it alone, outside the
             # lock, so neither the next round's kernels nor the other egress readers hold this thread up
-            if self.EGRESS_SPIN_S > 0:  # poll first (a blocking wait wakes up late on a ~30 us kernel)
-                t_end = time.perf_counter() + self.EGRESS_SPIN_S
-                while not wait.query() and time.perf_counter() < t_end:
-                    pass
             wait.synchronize()
             with self._egress_lock:
                 snap.pending = False
@@ -320,10 +315,6 @@ class TorchModelAdapter(ModelAdapterBase):
             snap.readers -= 1
             if snap.readers == 0 and snap is not self._snap:
                 self._snap_pool.append(snap.buf)
-
-    #: seconds get_weights() polls the event of a snapshot the round's kernel is still writing before it blocks on
-    #: it (0: block at once)
-    EGRESS_SPIN_S = 0.0
 
     #: models of at least this many bytes clone the snapshot with the native multi-threaded copy (fa_host_gather):
     #: one memcpy stream moves ~10 GB/s, so get_weights() of the headline's 100 MB model spent 10 of its 13 ms on
