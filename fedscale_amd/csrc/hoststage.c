@@ -13,50 +13,11 @@
 #include <Python.h>
 #define NPY_NO_DEPRECATED_API NPY_1_7_API_VERSION
 #include <numpy/arrayobject.h>
-#include <emmintrin.h>
-#include <stdint.h>
 #include <string.h>
-
-/* Non-temporal copies (the default): the staged rows are read by the GPU over PCIe (zero-copy) right after they are
- * written, so they go straight to DRAM with streaming stores instead of being left dirty in this core's cache for the
- * device's reads to snoop; one sfence per call orders them before the launch that follows.  0: plain memcpy. */
-static int g_nt = 1;
-
-static void copy_nt(char* d, const char* s, size_t n) {
-  if (n < 1024) {
-    memcpy(d, s, n);
-    return;
-  }
-  const size_t head = (16 - ((uintptr_t)d & 15)) & 15;
-  memcpy(d, s, head);
-  d += head;
-  s += head;
-  n -= head;
-  const size_t blocks = n / 64;
-  for (size_t i = 0; i < blocks; ++i) {
-    const __m128i a = _mm_loadu_si128((const __m128i*)(s + 0));
-    const __m128i b = _mm_loadu_si128((const __m128i*)(s + 16));
-    const __m128i c = _mm_loadu_si128((const __m128i*)(s + 32));
-    const __m128i e = _mm_loadu_si128((const __m128i*)(s + 48));
-    _mm_stream_si128((__m128i*)(d + 0), a);
-    _mm_stream_si128((__m128i*)(d + 16), b);
-    _mm_stream_si128((__m128i*)(d + 32), c);
-    _mm_stream_si128((__m128i*)(d + 48), e);
-    d += 64;
-    s += 64;
-  }
-  memcpy(d, s, n - blocks * 64);
-}
 
 #ifndef HS_BUILD_ID
 #define HS_BUILD_ID "unknown"
 #endif
-
-/* the result of a stage() call: every streaming store made so far is ordered before anything that follows */
-static PyObject* stop(Py_ssize_t i) {
-  if (g_nt) _mm_sfence();
-  return PyLong_FromSsize_t(i);
-}
 
 /* stage(values, dsts) -> int: copy values[i] into dsts[i] for every i (both lists of equal length) */
 static PyObject* hs_stage(PyObject* self, PyObject* args) {
@@ -71,36 +32,21 @@ static PyObject* hs_stage(PyObject* self, PyObject* args) {
   for (Py_ssize_t i = 0; i < n; ++i) {
     PyObject* a = PyList_GET_ITEM(values, i);
     PyObject* d = PyList_GET_ITEM(dsts, i);
-    if (!PyArray_CheckExact(a) || !PyArray_CheckExact(d)) return stop(i);
+    if (!PyArray_CheckExact(a) || !PyArray_CheckExact(d)) return PyLong_FromSsize_t(i);
     PyArrayObject* x = (PyArrayObject*)a;
     PyArrayObject* y = (PyArrayObject*)d;
     const int nd = PyArray_NDIM(y);
     if (PyArray_NDIM(x) != nd || PyArray_TYPE(x) != PyArray_TYPE(y) || !PyArray_ISNOTSWAPPED(x) ||
         !PyArray_IS_C_CONTIGUOUS(x) || !PyArray_IS_C_CONTIGUOUS(y) || !PyArray_ISWRITEABLE(y))
-      return stop(i);
+      return PyLong_FromSsize_t(i);
     const npy_intp* xs = PyArray_DIMS(x);
     const npy_intp* ys = PyArray_DIMS(y);
     for (int k = 0; k < nd; ++k)
-      if (xs[k] != ys[k]) return stop(i);
+      if (xs[k] != ys[k]) return PyLong_FromSsize_t(i);
     const npy_intp nbytes = PyArray_NBYTES(y);
-    if (nbytes) {
-      if (g_nt)
-        copy_nt((char*)PyArray_DATA(y), (const char*)PyArray_DATA(x), (size_t)nbytes);
-      else
-        memcpy(PyArray_DATA(y), PyArray_DATA(x), (size_t)nbytes);
-    }
+    if (nbytes) memcpy(PyArray_DATA(y), PyArray_DATA(x), (size_t)nbytes);
   }
-  return stop(-1);
-}
-
-/* set_nt(on) -> previous setting (A/B of the copy policy) */
-static PyObject* hs_set_nt(PyObject* self, PyObject* args) {
-  int on;
-  (void)self;
-  if (!PyArg_ParseTuple(args, "p", &on)) return NULL;
-  const int prev = g_nt;
-  g_nt = on;
-  return PyBool_FromLong(prev);
+  return PyLong_FromLong(-1);
 }
 
 static PyObject* hs_build_id(PyObject* self, PyObject* noargs) {
@@ -111,7 +57,6 @@ static PyObject* hs_build_id(PyObject* self, PyObject* noargs) {
 
 static PyMethodDef hs_methods[] = {
     {"stage", hs_stage, METH_VARARGS, "stage(values, dsts) -> -1, or the index of the first entry left to Python"},
-    {"set_nt", hs_set_nt, METH_VARARGS, "set_nt(on) -> previous: streaming (non-temporal) copies on or off"},
     {"build_id", hs_build_id, METH_NOARGS, "the build id of this module's source (fedscale_amd/buildinfo.py)"},
     {NULL, NULL, 0, NULL}};
 

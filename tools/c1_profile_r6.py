@@ -81,23 +81,18 @@ def main():
     rows = run_rounds(agg, K, ups)
     print(json.dumps({"round_unwrapped_us": med(rows, "round")}), flush=True)
     # the drop-in's round with each knob off in turn (A/B of this round's changes), interleaved
-    from fedscale_amd import hoststage
-
-    hs = hoststage.load()
-    knobs = {"all_on": {}, "head_launch_off": {"SPLIT": False}, "plain_copies": {"NT": False}}
+    knobs = {"all_on": {}, "small_finish_off": {"SMALL_ROUND_FINISH": False}, "head_launch_off": {"SPLIT": False}}
     res = {k: [] for k in knobs}
     aggs = {k: make(dev) for k in knobs}
     for rep in range(6):
         for k, kv in knobs.items():
             a, KK, u = aggs[k]
             for attr, v in kv.items():
-                if attr not in ("SPLIT", "NT"):
+                if attr != "SPLIT":
                     setattr(a.model_wrapper, attr, v)
             rd.DeviceRound.SPLIT_SMALL_ROUNDS = kv.get("SPLIT", True)
-            hs.set_nt(kv.get("NT", True))
             rows = run_rounds(a, KK, u, n=100, warm=10)
             rd.DeviceRound.SPLIT_SMALL_ROUNDS = True
-            hs.set_nt(True)
             res[k].append(med(rows, "round"))
     print(json.dumps({"ab_round_us": {k: sorted(v) for k, v in res.items()}}), flush=True)
     # as bench.py runs it: the main thread bound to the GPU's NUMA node (hostnuma.bind_to_gpu), and bench's own round
