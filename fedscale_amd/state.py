@@ -350,6 +350,7 @@ def spmd_rccl_probe(device_index: int, group=None, timeout_s: float = 90.0) -> d
     hangs is killed at the deadline, and every rank then reaches the same all_gather of (ok, result | error), so the
     ranks always leave together, with the failures named."""
     import ctypes
+    import json
     import os
     import subprocess
     import sys
@@ -381,7 +382,7 @@ def spmd_rccl_probe(device_index: int, group=None, timeout_s: float = 90.0) -> d
     try:
         r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=timeout_s)
         lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-        mine = __import__("json").loads(lines[-1]) if lines else {
+        mine = json.loads(lines[-1]) if lines else {
             "ok": False, "error": "rc %s: %s" % (r.returncode, r.stderr[-300:])}
     except subprocess.TimeoutExpired:
         mine = {"ok": False, "error": f"no result within {timeout_s:g} s (ncclCommInitRank did not complete)"}
