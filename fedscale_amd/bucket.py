@@ -422,11 +422,15 @@ class ClientStaging:
         ev.record(stream)
         return ev
 
+    def put_small(self, slot: int, update: dict) -> bool:
+        """A small whole-model upload (a dict, config 1) into its slot of the pinned mirror; False: not taken (the
+        caller goes on with ``put``, which converts or raises as for any upload)."""
+        values = list(update.values())
+        return len(values) == self.layout.T and self._put_bulk_views(slot, values)
+
     def put(self, slot: int, update):
-        if self._views is not None and type(update) is dict:  # a small whole-model upload (config 1): the common case
-            values = list(update.values())
-            if len(values) == self.layout.T and self._put_bulk_views(slot, values):
-                return
+        if self._views is not None and type(update) is dict and self.put_small(slot, update):
+            return  # a small whole-model upload (config 1): the common case
         if type(update) is HostRow:
             return self._put_row(slot, update)
         if type(update) is RegisteredUpload:

@@ -25,6 +25,7 @@ import numpy as np
 import torch
 
 from ...bucket import BucketLayout, ClientStaging
+from ... import hoststage
 from ... import kernels as kx
 from ..._native import FA_ACCUMULATE, FA_FINALIZE
 from ...kernels import qfed_max_chunk as kx_qfed_max_chunk
@@ -90,7 +91,7 @@ class _HostBuf:
     """Pinned host buffers for one model version (fp32 bucket ``f``, side table ``s``) with their state_dict
     views, made once: buffers are pooled across versions, so egress clones from ready-made views."""
 
-    __slots__ = ("f", "s", "views", "np_views", "ev")
+    __slots__ = ("f", "s", "views", "np_views", "np_list", "ev")
 
     def __init__(self, layout: BucketLayout):
         # round_up(P, 4) floats: fa_reduce_mirror writes whole float4 columns into ``f``
@@ -98,6 +99,7 @@ class _HostBuf:
         self.s = torch.empty(max(1, layout.Q), dtype=torch.int64)
         self.views = layout.unpack(self.f, self.s)
         self.np_views = [v.numpy() for v in self.views]
+        self.np_list = list(self.np_views)  # (hoststage.stage takes a list)
         # recorded after the kernel that writes this buffer (fa_reduce_mirror); re-recorded only while the buffer
         # is out of the pool, i.e. while no reader can be waiting on it
         self.ev = torch.cuda.Event()
@@ -350,13 +352,31 @@ class TorchModelAdapter(ModelAdapterBase):
         if getattr(_HANDLE_ONCE, "adapter", None) is self:  # the caller only serialises this list
             _HANDLE_ONCE.adapter = None
             return self.egress_handle()
+        pre = self._preallocate_clones()  # (small models) before the wait for the round's kernel, which hides it
         snap = self._acquire_host()
         try:
-            out = EgressWeights(self._clone_weights(snap))
+            if pre is not None and hoststage.stage(snap.buf.np_list, pre[0]) < 0:
+                out = EgressWeights(pre[1])
+            else:
+                out = EgressWeights(self._clone_weights(snap))
             out.egress_key = (self._egress_id, snap.version)
         finally:
             self._release_host(snap)
         return out
+
+    def _preallocate_clones(self):
+        """(numpy arrays, the CPU tensors over them) for the clones of a small model (below CLONE_PARALLEL_MIN_BYTES):
+        fresh, independent storage per call, as ``params.data.clone()`` gives (torch_model_adapter.py:47).  Made
+        before get_weights() waits for a round's kernel, they cost nothing on the round's critical path; the copy
+        after the wait is one native call (fedscale_amd/csrc/hoststage.c) over all of them."""
+        L = self.layout
+        if L.P_full * 4 >= self.CLONE_PARALLEL_MIN_BYTES:
+            return None
+        specs = self.__dict__.get("_clone_specs")
+        if specs is None:
+            specs = self._clone_specs = [(e.shape, np.float32 if e.kind == "f" else np.int64) for e in L.entries]
+        arrs = [np.empty(shape, dtype) for shape, dtype in specs]
+        return arrs, [torch.from_numpy(a) for a in arrs]
 
     def egress_bytes(self, key) -> Optional[bytes]:
         """``pickle.dumps`` of get_weights() for model version ``key`` — the bytes the reference's

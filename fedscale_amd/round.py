@@ -139,6 +139,9 @@ class DeviceRound:
         self.head = 0  # arrivals [0, head) already reduced into head_acc by the head launch (_launch_head)
         self.head_acc = None
         self._split_at = self._head_split()
+        # FedAvg rounds of a whole-model layout staged in a pinned mirror take add()'s short path
+        self._small = (policy == "fedavg" and self.cg is None and self.staging.bulk
+                       and self.staging._views is not None)
 
     #: small zero-copy FedAvg rounds (config 1) reduce their first half while the second half is still arriving
     #: (``_launch_head``); False: one finishing launch over every row
@@ -193,6 +196,17 @@ class DeviceRound:
     def add(self, update, *, weight: Optional[float] = None, loss: Optional[float] = None,
             learning_rate: Optional[float] = None, q: Optional[float] = None):
         """Stage one arriving client update (in arrival order)."""
+        if self._small and type(update) is dict and self.n < self.K and self.slot < self.cap:
+            # a small FedAvg round's upload straight into its slot of the pinned mirror (config 1; anything the
+            # native copy does not take, or an error, goes on below and is handled — or raised — as before)
+            slot = self.slot
+            if self.staging.put_small(slot, update):
+                self.slot = slot + 1
+                self.n += 1
+                self.n_local += 1
+                if self.slot == self._split_at:
+                    self._launch_head()
+                return
         if self.n >= self.K:
             raise RuntimeError(f"round already has its K={self.K} results")
         if not (self.k_begin <= self.n < self.k_end):  # another rank's client (client mode)

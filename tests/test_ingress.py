@@ -280,6 +280,9 @@ def test_client_ping_update_model_hands_out_the_egress_handle():
         def egress_handle(self):
             return "HANDLE"
 
+        def _preallocate_clones(self):
+            return None
+
         def _acquire_host(self):
             self.clones += 1
             raise LookupError("clone path")
