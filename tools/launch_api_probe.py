@@ -36,7 +36,14 @@ def main():
     def launch():
         return lib.fa_reduce_mirror(hx.data_ptr(), ld, K, P, None, None, out.data_ptr(), mir.data_ptr(), denom, 2, st)
 
+    tev.record(s)
+    torch.cuda.synchronize(dev)
+    nullst = torch.cuda.default_stream(dev)
+    other = torch.cuda.Stream(device=dev)
     follow = {
+        "null_stream_wait_event_torch": lambda: nullst.wait_event(tev),
+        "null_stream_wait_event_raw": lambda: hip.hipStreamWaitEvent(ctypes.c_void_p(0), ctypes.c_void_p(tev.cuda_event), 0),
+        "pool_stream_wait_event_torch": lambda: other.wait_event(tev),
         "torch_event_record": lambda: tev.record(s),
         "raw_hipEventRecord": lambda: hip.hipEventRecord(raw, ctypes.c_void_p(st)),
         "hipStreamQuery": lambda: hip.hipStreamQuery(ctypes.c_void_p(st)),
@@ -50,6 +57,8 @@ def main():
                 torch.cuda.synchronize(dev)
                 if after_launch:
                     launch()
+                    if "wait_event" in name:  # the event of that launch, as the adapter's join waits on
+                        tev.record(s)
                 t0 = time.perf_counter()
                 fn()
                 t1 = time.perf_counter()
