@@ -1146,14 +1146,13 @@ def main():
     split_ms = getattr(w, "split_ms", None)  # FedYoGi: (k_reduce ms, k_yogi_step ms) per step
     # (launches: of the dominant kernel per step; fa_reduce runs long buckets as column windows (fedagg.hip
     # FA_WINDOWS), so the per-launch figures rocprof reports are the step's divided by it)
-    w.free()
-    del w
-
     drop_in = None
     if world == 1 and policy == "fedavg" and not weak and not args.no_other_configs:
         # the same round through the drop-in (TorchModelAdapter begin_round / apply_round, every launch on the part's
         # stream) with the N > 1 line's in-process timing (fedscale_amd.inproc_bench): value(N) / value_drop_in(1)
-        # then compares one methodology; outside the timed region, never `value`
+        # then compares one methodology; outside the timed region, never `value`.  Run while the headline's
+        # inputs are still allocated, so its staging is fresh memory as the headline's was (allocated after the
+        # headline's 100 GB were freed it read 3-4 % slower, r06_bench_default_n1.json / the verification line)
         from fedscale_amd.inproc_bench import run_one
 
         try:
@@ -1162,6 +1161,9 @@ def main():
             drop_in = run_one(local_dev, K, P, rounds=args.steps, warmup=max(30, warmup_used), seed=args.seed)
         except Exception as e:  # reported, never fatal
             drop_in = {"error": f"{type(e).__name__}: {e}"}
+
+    w.free()
+    del w
 
     other = None
     if not args.no_other_configs and args.config == "headline":
