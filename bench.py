@@ -1146,6 +1146,23 @@ def main():
     split_ms = getattr(w, "split_ms", None)  # FedYoGi: (k_reduce ms, k_yogi_step ms) per step
     # (launches: of the dominant kernel per step; fa_reduce runs long buckets as column windows (fedagg.hip
     # FA_WINDOWS), so the per-launch figures rocprof reports are the step's divided by it)
+    one_gpu = inproc = None
+    if world > 1 and strong and not args.no_selfcheck:
+        # outside the timed region, the other ranks waiting at a host-side barrier (gloo: an RCCL barrier would park
+        # a spinning kernel on their GPUs while rank 0's child uses them): (1) the same round on one GPU over the
+        # whole model, so the line carries its own scaling reference; (2) the in-process drop-in timed over the
+        # node's GPUs — what a FedScale deployment runs (one aggregator process), and the N > 1 line's `value`.
+        # Both run before any rank frees its inputs: a 100 GB buffer allocated into memory freed buffers held reads
+        # 3-4 % slower than one allocated fresh, whichever path reads it (profiles/r06_alloc_reuse_probe.log), and
+        # the headline's own inputs were allocated fresh
+        _sync_all(dev, world)
+        dist.barrier(group=cpu_group)
+        if rank == 0:
+            one_gpu = one_gpu_reference(policy, K, P, dev, args.seed)
+            if policy == "fedavg":
+                inproc = run_inproc_bench(world, K, P, args.dist_backend, steps=args.steps, warmup=warmup_used)
+        dist.barrier(group=cpu_group)
+
     drop_in = None
     if world == 1 and policy == "fedavg" and not weak and not args.no_other_configs:
         # the same round through the drop-in (TorchModelAdapter begin_round / apply_round, every launch on the part's
@@ -1175,20 +1192,6 @@ def main():
                     "c4", CONFIGS["c4"], dev, rank, world, shards, args.seed, args.dist_backend),
                 f"c5_qfedavg_k10000_p100M_x{world}": config_line(
                     "c5", CONFIGS["c5"], dev, rank, world, shards, args.seed, args.dist_backend, steps=2, warmup=1)}
-
-    one_gpu = inproc = None
-    if world > 1 and strong and not args.no_selfcheck:
-        # outside the timed region, the other ranks waiting at a host-side barrier (gloo: an RCCL barrier would park
-        # a spinning kernel on their GPUs while rank 0's child uses them): (1) the same round on one GPU over the
-        # whole model, so the line carries its own scaling reference; (2) the in-process drop-in timed over the
-        # node's GPUs — what a FedScale deployment runs (one aggregator process), and the N > 1 line's `value`
-        _sync_all(dev, world)
-        dist.barrier(group=cpu_group)
-        if rank == 0:
-            one_gpu = one_gpu_reference(policy, K, P, dev, args.seed)
-            if policy == "fedavg":
-                inproc = run_inproc_bench(world, K, P, args.dist_backend, steps=args.steps, warmup=warmup_used)
-        dist.barrier(group=cpu_group)
 
     selfcheck = None
     if world > 1 and not args.no_selfcheck and args.dist_backend == "nccl":
