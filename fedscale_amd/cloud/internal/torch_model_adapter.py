@@ -130,7 +130,9 @@ class TorchModelAdapter(ModelAdapterBase):
     """``dstream``: the ``DeviceStream`` (GPU + HIP stream) every kernel, copy and event of this adapter is
     issued on — made for ``device`` when not given; a ``ShardedModelAdapter`` hands each part its own.  Each
     public call runs under ``dstream.joined()``: the adapter's GPU is current for the call (whatever the
-    caller had current) and the caller's stream on that GPU is ordered after the call's work."""
+    caller had current) and the caller's stream on that GPU is ordered after the call's work — except
+    ``apply_round`` of a round that exposes no device state (``_round_exposes_device_state``), whose results every
+    public reader waits for by itself."""
 
     def __init__(self, model: torch.nn.Module, optimizer=None, device=None, shards: Optional[ShardGroup] = None,
                  staging_capacity: Optional[int] = None, _load_from=None, dstream: Optional[DeviceStream] = None):
@@ -479,8 +481,22 @@ class TorchModelAdapter(ModelAdapterBase):
                     keep_mean: bool = True):
         """Finish a round: reduce the last chunk with the server step fused, then swap buffers."""
         self._commit_ev = None
-        with self.dstream.joined(self._take_commit_event):
-            self._apply_round(rnd, denom32, denom64, keep_mean)
+        if self._round_exposes_device_state():
+            with self.dstream.joined(self._take_commit_event):
+                self._apply_round(rnd, denom32, denom64, keep_mean)
+        else:
+            with self.dstream:
+                self._apply_round(rnd, denom32, denom64, keep_mean)
+
+    def _round_exposes_device_state(self) -> bool:
+        """Whether a round leaves device buffers a caller can read through the public API — the FedYoGi optimizer's
+        ``m_t`` / ``v_t`` (device views, yogi.py's reference attributes) — so the caller's stream must be ordered
+        after the round (DeviceStream.joined).  Otherwise every public reader of the round's results is ordered
+        by the adapter itself (get_weights / egress wait on the round's event, model_weights reads on the adapter's
+        stream), and the join — a hipStreamWaitEvent on a kernel still running, 5 us against 0.5 us on an idle one
+        (profiles/r06_launch_api_probe.log), ~6 % of config 1's round — is skipped."""
+        opt = self.optimizer
+        return opt is not None and getattr(opt, "mode", None) == "fed-yogi"
 
     def _take_commit_event(self):
         """The event ``_commit_scratch`` recorded for the round just applied (after all of its work on the

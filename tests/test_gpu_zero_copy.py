@@ -243,3 +243,44 @@ def test_head_launch_keeps_every_bit(gpu_device, monkeypatch, K, small_finish):
     for r in range(3):
         for a, b in zip(got[(True, r)], got[(False, r)]):
             assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("policy", [None, "fed-yogi"])
+def test_apply_round_joins_the_caller_only_when_device_state_is_exposed(gpu_device, monkeypatch, policy):
+    """Round 6: apply_round orders the caller's stream after the round (a hipStreamWaitEvent) only when the round
+    leaves device state a caller can read through the API (FedYoGi's m_t / v_t); FedAvg's results are read through
+    get_weights / model_weights, which wait for the round themselves.  Both stay exact."""
+    import argparse
+
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.aggregation.optimizers import TorchServerOptimizer
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+    from fedscale_amd.state import DeviceStream
+
+    names, tensors, _, _ = _femnist_adapter(gpu_device)
+    args = argparse.Namespace(gradient_policy=policy, yogi_eta=3e-3, yogi_tau=1e-8, yogi_beta=0.9, yogi_beta2=0.99)
+    adapter = TorchModelAdapter(StateDictModule(names, [t.clone() for t in tensors]), device=gpu_device,
+                                optimizer=TorchServerOptimizer(policy, args, gpu_device))
+    agg = DeviceAggregator(adapter, args)
+    joins, real = [], DeviceStream._exit
+
+    def spy(self, join, done=None):
+        joins.append(join)
+        return real(self, join, done)
+
+    monkeypatch.setattr(DeviceStream, "_exit", spy)
+    ups = _uploads(names, tensors, 6, 9)
+    agg.start_round(6)
+    for k, u in enumerate(ups[:-1]):
+        agg.on_result({"client_id": k, "update_weight": u, "moving_loss": 1.0})
+    del joins[:]
+    agg.on_result({"client_id": 5, "update_weight": ups[-1], "moving_loss": 1.0})  # the round's apply_round
+    assert (True in joins) == (policy == "fed-yogi"), joins
+    if policy is None:
+        assert_state_equal(adapter.get_weights(), _oracle_round(ups), "FedAvg after an unjoined round")
+        m = np.concatenate([np.asarray(w, np.float32).reshape(-1) for w in agg.model_weights])
+        want = np.concatenate([w.reshape(-1) for w in _oracle_round(ups)])
+        np.testing.assert_array_equal(m, want)
+    else:
+        y = adapter.optimizer.gradient_controller
+        assert torch.isfinite(torch.cat([t.reshape(-1).cpu() for t in y.m_t])).all()  # read on the caller's stream
