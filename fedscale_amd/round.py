@@ -143,9 +143,11 @@ class DeviceRound:
         self._small = (policy == "fedavg" and self.cg is None and self.staging.bulk
                        and self.staging._views is not None)
 
-    #: small zero-copy FedAvg rounds (config 1) reduce their first half while the second half is still arriving
+    #: small zero-copy FedAvg rounds (config 1) reduce their first arrivals while the rest are still arriving
     #: (``_launch_head``); False: one finishing launch over every row
     SPLIT_SMALL_ROUNDS = True
+    #: the share of the K arrivals the head launch reduces (the rest: the finishing launch)
+    SPLIT_FRACTION = 0.5
 
     def _head_split(self):
         """The arrival count after which the head launch goes out (None: this round takes no head launch): FedAvg
@@ -156,7 +158,7 @@ class DeviceRound:
                 or self.cap < self.K or self.dstream is None or L.Q or not st.bulk or st._views is None
                 or self.K * (L.ld * 4 + L.ldq * 8) > st.ZERO_COPY_MAX_BYTES):
             return None
-        return self.K // 2
+        return min(self.K - 1, max(1, int(self.K * self.SPLIT_FRACTION)))
 
     def _launch_head(self):
         """Reduce the arrivals staged so far, [0, slot), straight out of the pinned mirror into ``head_acc`` (the

@@ -118,12 +118,15 @@ def test_config1_rounds_read_the_mirror_and_write_egress(gpu_device, monkeypatch
         mir = [c for c in calls if c[0] == "fa_reduce_mirror"]
         head = [c for c in calls if c[0] == "fa_reduce"]
         assert len(mir) == 1 and len(head) == 1, [c[0] for c in calls]
-        # round 6: the first 5 arrivals are reduced out of the mirror while the last 5 arrive (DeviceRound
-        # _launch_head: raw chain, no finalize), the finishing launch continues the chain over rows 5..9
+        # round 6: the first m arrivals are reduced out of the mirror while the rest arrive (DeviceRound
+        # _launch_head: raw chain, no finalize), the finishing launch continues the chain over rows m..9
+        from fedscale_amd.round import DeviceRound
+
+        m = min(9, max(1, int(10 * DeviceRound.SPLIT_FRACTION)))  # the head launch's share of the 10 arrivals
         hx, ld = adapter.staging._hx, adapter.staging._hx.shape[1]
-        assert head[0][1][0] == hx.data_ptr() and head[0][1][2] == 5 and head[0][1][8] == 0
-        assert mir[0][1][0] == hx.data_ptr() + 5 * ld * 4, "the reduce did not read the pinned mirror"
-        assert mir[0][1][2] == 5 and mir[0][1][5] == head[0][1][6], "the finish does not continue the head's chain"
+        assert head[0][1][0] == hx.data_ptr() and head[0][1][2] == m and head[0][1][8] == 0
+        assert mir[0][1][0] == hx.data_ptr() + m * ld * 4, "the reduce did not read the pinned mirror"
+        assert mir[0][1][2] == 10 - m and mir[0][1][5] == head[0][1][6], "the finish does not continue the head's chain"
         assert mir[0][1][7] == adapter._snap.buf.f.data_ptr(), "the mean was not written into the snapshot"
         want = _oracle_round(ups)
         assert_state_equal(adapter.get_weights(), want, f"round {r}")

@@ -81,18 +81,21 @@ def main():
     rows = run_rounds(agg, K, ups)
     print(json.dumps({"round_unwrapped_us": med(rows, "round")}), flush=True)
     # the drop-in's round with each knob off in turn (A/B of this round's changes), interleaved
-    knobs = {"all_on": {}, "small_finish_off": {"SMALL_ROUND_FINISH": False}, "head_launch_off": {"SPLIT": False}}
+    knobs = {"all_on": {}, "head_launch_off": {"SPLIT": False}, "split_0.6": {"FRAC": 0.6}, "split_0.7": {"FRAC": 0.7},
+             "split_0.4": {"FRAC": 0.4}}
     res = {k: [] for k in knobs}
     aggs = {k: make(dev) for k in knobs}
     for rep in range(6):
         for k, kv in knobs.items():
             a, KK, u = aggs[k]
             for attr, v in kv.items():
-                if attr != "SPLIT":
+                if attr not in ("SPLIT", "FRAC"):
                     setattr(a.model_wrapper, attr, v)
             rd.DeviceRound.SPLIT_SMALL_ROUNDS = kv.get("SPLIT", True)
+            rd.DeviceRound.SPLIT_FRACTION = kv.get("FRAC", 0.5)
             rows = run_rounds(a, KK, u, n=100, warm=10)
             rd.DeviceRound.SPLIT_SMALL_ROUNDS = True
+            rd.DeviceRound.SPLIT_FRACTION = 0.5
             res[k].append(med(rows, "round"))
     print(json.dumps({"ab_round_us": {k: sorted(v) for k, v in res.items()}}), flush=True)
     # as bench.py runs it: the main thread bound to the GPU's NUMA node (hostnuma.bind_to_gpu), and bench's own round
