@@ -81,8 +81,8 @@ def main():
     rows = run_rounds(agg, K, ups)
     print(json.dumps({"round_unwrapped_us": med(rows, "round")}), flush=True)
     # the drop-in's round with each knob off in turn (A/B of this round's changes), interleaved
-    knobs = {"all_on": {}, "head_launch_off": {"SPLIT": False}, "split_0.6": {"FRAC": 0.6}, "split_0.7": {"FRAC": 0.7},
-             "split_0.4": {"FRAC": 0.4}}
+    knobs = {"all_on": {}, "head_launch_off": {"SPLIT": False}, "split_0.7": {"FRAC": 0.7}, "split_0.8": {"FRAC": 0.8},
+             "split_0.9": {"FRAC": 0.9}}
     res = {k: [] for k in knobs}
     aggs = {k: make(dev) for k in knobs}
     for rep in range(6):
