@@ -146,8 +146,10 @@ class DeviceRound:
     #: small zero-copy FedAvg rounds (config 1) reduce their first arrivals while the rest are still arriving
     #: (``_launch_head``); False: one finishing launch over every row
     SPLIT_SMALL_ROUNDS = True
-    #: the share of the K arrivals the head launch reduces (the rest: the finishing launch)
-    SPLIT_FRACTION = 0.5
+    #: the share of the K arrivals the head launch reduces (the rest: the finishing launch).  Config 1 (K = 10) per
+    #: round: 0.5 81.3-82.9 us, 0.7 76.7-78.3, 0.8 77.3-81.2, 0.9 79.6-84.6 (profiles/r06_c1_profile_split2.log): the
+    #: head kernel's PCIe reads finish behind the last arrivals' staging, and the finishing launch reads less
+    SPLIT_FRACTION = 0.7
 
     def _head_split(self):
         """The arrival count after which the head launch goes out (None: this round takes no head launch): FedAvg

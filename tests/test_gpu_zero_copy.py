@@ -221,7 +221,7 @@ def test_pointer_kinds_and_pageable_rejection(gpu_device):
 @pytest.mark.parametrize("small_finish", [True, False], ids=["finish_small", "finish_general"])
 @pytest.mark.parametrize("K", [1, 3, 4, 5, 7, 10, 16])
 def test_head_launch_keeps_every_bit(gpu_device, monkeypatch, K, small_finish):
-    """Round 6: small zero-copy FedAvg rounds reduce their first K // 2 arrivals while the rest arrive
+    """Round 6: small zero-copy FedAvg rounds reduce their first arrivals (SPLIT_FRACTION of K) while the rest arrive
     (DeviceRound._launch_head) and finish with the chain continued from that partial sum — through the small-round
     finish or DeviceRound.finalize_mean; the model is the oracle's, bit for bit, and the same as with one finishing
     launch over all rows, for every K (K < 4: no head launch)."""
