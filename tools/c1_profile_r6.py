@@ -84,6 +84,7 @@ def main():
     knobs = {"all_on": {}, "head_launch_off": {"SPLIT": False}, "split_0.7": {"FRAC": 0.7}, "split_0.8": {"FRAC": 0.8},
              "split_0.9": {"FRAC": 0.9}}
     res = {k: [] for k in knobs}
+    frac0 = rd.DeviceRound.SPLIT_FRACTION  # "all_on": the product default
     aggs = {k: make(dev) for k in knobs}
     for rep in range(6):
         for k, kv in knobs.items():
@@ -92,10 +93,10 @@ def main():
                 if attr not in ("SPLIT", "FRAC"):
                     setattr(a.model_wrapper, attr, v)
             rd.DeviceRound.SPLIT_SMALL_ROUNDS = kv.get("SPLIT", True)
-            rd.DeviceRound.SPLIT_FRACTION = kv.get("FRAC", 0.5)
+            rd.DeviceRound.SPLIT_FRACTION = kv.get("FRAC", frac0)
             rows = run_rounds(a, KK, u, n=100, warm=10)
             rd.DeviceRound.SPLIT_SMALL_ROUNDS = True
-            rd.DeviceRound.SPLIT_FRACTION = 0.5
+            rd.DeviceRound.SPLIT_FRACTION = frac0
             res[k].append(med(rows, "round"))
     print(json.dumps({"ab_round_us": {k: sorted(v) for k, v in res.items()}}), flush=True)
     # as bench.py runs it: the main thread bound to the GPU's NUMA node (hostnuma.bind_to_gpu), and bench's own round
