@@ -1284,6 +1284,12 @@ def main():
                             "kernel_ms_per_rank": kern_ms_ranks, "kernel_ms_max": kern_ms_max,
                             "kernel_ms_rank0": kern_ms, "rccl": rccl_probe,
                             "roofline_from": "max over ranks of the dominant kernel's mean time per step"}
+            n_visible = torch.cuda.device_count()
+            if args.dist_backend != "nccl" or n_visible < world:
+                # a rehearsal: ranks (and the in-process parts) share the visible GPU(s), so no rate on this line is
+                # an N-GPU rate (SCALE-shaped JSON must not read as scaling data)
+                res["plumbing_only"] = (f"{world} ranks on {min(n_visible, world)} GPU(s), backend {args.dist_backend}: "
+                                        "every rate on this line is plumbing, not an N-GPU measurement")
         if reassembly_ms is not None:
             # every round ends in egress (aggregator.py:788-804): the model reassembled from the shards
             res["reassembly_ms"] = reassembly_ms

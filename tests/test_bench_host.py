@@ -187,3 +187,5 @@ def test_committed_rehearsal_lines_are_complete():
         line = json.loads([ln for ln in open(p).read().splitlines() if ln.startswith("{")][-1])
         assert line["n_gpus"] > 1 and bench.check_line(line) == [], (p, bench.check_line(line))
         assert line["schema"]["complete"] and "plumbing" in json.dumps(line["pcie_inclusive"])
+        if "plumbing_only" in line:  # (lines from round 6's last bench.py carry the machine-readable flag)
+            assert "plumbing" in line["plumbing_only"] and "spmd" in line["value_source"]
