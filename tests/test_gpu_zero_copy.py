@@ -287,3 +287,50 @@ def test_apply_round_joins_the_caller_only_when_device_state_is_exposed(gpu_devi
     else:
         y = adapter.optimizer.gradient_controller
         assert torch.isfinite(torch.cat([t.reshape(-1).cpu() for t in y.m_t])).all()  # read on the caller's stream
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_small_rounds_random_layouts_bit_exact(gpu_device, seed):
+    """Small whole-model FedAvg rounds on random layouts (1-6 fp32 tensors, odd sizes, 0-d included) and random K:
+    the native staging, the head launch at SPLIT_FRACTION of K and the small-round finish give the oracle's model bit for
+    bit, round after round on the same adapter (the staging, the head accumulator and the snapshots reused)."""
+    from fedscale_amd.cloud.aggregation.aggregator import DeviceAggregator
+    from fedscale_amd.cloud.internal.torch_model_adapter import TorchModelAdapter
+
+    rng = np.random.default_rng(1000 + seed)
+    T = int(rng.integers(1, 7))
+    shapes = [tuple(int(d) for d in rng.integers(1, 60, size=int(rng.integers(0, 4)))) for _ in range(T)]
+    names = [f"t{i}" for i in range(T)]
+    tensors = [torch.from_numpy(rng.standard_normal(s).astype(np.float32)) for s in shapes]
+    adapter = TorchModelAdapter(StateDictModule(names, tensors), device=gpu_device)
+    agg = DeviceAggregator(adapter)
+    for r in range(3):
+        K = int(rng.integers(2, 25))
+        ups = _uploads(names, tensors, K, 10 * seed + r)
+        agg.start_round(K)
+        for k, u in enumerate(ups):
+            agg.on_result({"client_id": k, "update_weight": u, "moving_loss": 1.0})
+        assert_state_equal(adapter.get_weights(), _oracle_round(ups), f"seed {seed} round {r} K={K}")
+
+
+def test_small_round_bad_upload_raises_as_before(gpu_device):
+    """An upload the native staging does not take is handed to the Python path, which converts or raises exactly as
+    before: a wrong shape raises ValueError naming the entry, a wrong dtype TypeError; a list upload and float64
+    arrays (converted by the general path as numpy would) still give the oracle's model."""
+    names, tensors, adapter, agg = _femnist_adapter(gpu_device)
+    ups = _uploads(names, tensors, 4, 77)
+    agg.start_round(4)
+    bad = dict(ups[0])
+    bad[names[2]] = bad[names[2]].reshape(-1)
+    with pytest.raises(ValueError, match=names[2]):
+        agg.on_result({"client_id": 0, "update_weight": bad, "moving_loss": 1.0})
+    agg.model_in_update -= 1  # (the reference would have died here; undo the caller's count to go on)
+    bad = dict(ups[0])
+    bad[names[0]] = bad[names[0]].astype(np.float16)
+    with pytest.raises(TypeError, match=names[0]):
+        agg.on_result({"client_id": 0, "update_weight": bad, "moving_loss": 1.0})
+    agg.model_in_update -= 1
+    agg.on_result({"client_id": 0, "update_weight": list(ups[0].values()), "moving_loss": 1.0})
+    for k, u in enumerate(ups[1:], 1):
+        agg.on_result({"client_id": k, "update_weight": u, "moving_loss": 1.0})
+    assert_state_equal(adapter.get_weights(), _oracle_round(ups), "after refused uploads")
