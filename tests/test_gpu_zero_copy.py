@@ -315,8 +315,8 @@ def test_small_rounds_random_layouts_bit_exact(gpu_device, seed):
 
 def test_small_round_bad_upload_raises_as_before(gpu_device):
     """An upload the native staging does not take is handed to the Python path, which converts or raises exactly as
-    before: a wrong shape raises ValueError naming the entry, a wrong dtype TypeError; a list upload and float64
-    arrays (converted by the general path as numpy would) still give the oracle's model."""
+    before: a wrong shape raises ValueError naming the entry, a wrong dtype TypeError (retrying the slot then works);
+    a list upload still gives the oracle's model."""
     names, tensors, adapter, agg = _femnist_adapter(gpu_device)
     ups = _uploads(names, tensors, 4, 77)
     agg.start_round(4)
